@@ -1,0 +1,413 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the reference polarcub itself.
+
+TEST INFRASTRUCTURE ONLY -- runs in the build container, never on the GPU box
+(the reference tree does not exist there).  It imports /root/reference
+in-process, with bytecode writing disabled, and applies two runtime shims
+(no reference file is edited or copied):
+
+  1. np.float / np.int / np.product aliases: the q-ary code still uses the
+     NumPy < 1.24 names (VectorDistributions/QaryMemorylessVectorDistribution.py:16,72).
+  2. normalizeDistList = normalize on the binary vector-distribution classes:
+     BinaryPolarEncoderDecoder.py:279,285,299,305 call a method no class defines.
+
+Outputs small .npz fixtures into tests/golden/ together with ref_timing.json.
+Every fixture records its seeds and construction choices in a `meta` string.
+
+Usage:  python oracle/make_golden.py [--only NAME ...]
+"""
+import argparse
+import json
+import math
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+
+
+def load_reference():
+    if not os.path.isdir(REF):
+        sys.exit("make_golden.py: /root/reference is not present (this script only runs in the build container)")
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    np.float = float  # noqa: shim 1
+    np.int = int
+    np.product = np.prod
+    import BinaryPolarEncoderDecoder as BPED
+    import QaryPolarEncoderDecoder as QPED
+    from ScalarDistributions import BinaryMemorylessDistribution as BMD
+    from ScalarDistributions import QaryMemorylessDistribution as QMD
+    from VectorDistributions import BinaryMemorylessVectorDistribution as BMVD
+    from VectorDistributions import BinaryTrellis as BT
+    from VectorDistributions import CollectionOfBinaryTrellises as CBT
+    from VectorDistributions import QaryMemorylessVectorDistribution as QMVD
+    for cls in (BMVD.BinaryMemorylessVectorDistribution, BT.BinaryTrellis, CBT.CollectionOfBinaryTrellises):
+        cls.normalizeDistList = cls.normalize  # shim 2
+    return dict(BPED=BPED, QPED=QPED, BMD=BMD, QMD=QMD, BMVD=BMVD, BT=BT, CBT=CBT, QMVD=QMVD)
+
+
+# ---------------------------------------------------------------------------
+# helpers (build-side code, not reference code)
+# ---------------------------------------------------------------------------
+
+def bhattacharyya_frozen(n, K, sigma2):
+    """Frozen set = the N-K least reliable indices by the Bhattacharyya recursion
+    for BI-AWGN, in the adjacent-pair index convention (minus child = 2j, plus = 2j+1
+    at each level, so u = path bits MSB first)."""
+    z = np.array([math.exp(-1.0 / (2.0 * sigma2))])
+    for _ in range(n):
+        nz = np.empty(2 * len(z))
+        nz[0::2] = 2 * z - z * z
+        nz[1::2] = z * z
+        z = nz
+    order = sorted(range(len(z)), key=lambda i: (z[i], i))  # most reliable first
+    info = set(order[:K])
+    return set(i for i in range(len(z)) if i not in info), z
+
+
+def awgn_pairs(x, sigma2, rng):
+    """Joint P(x, y) for BPSK 0->+1, 1->-1 over AWGN with variance sigma2."""
+    s = 1.0 - 2.0 * x.astype(np.float64)
+    y = s + math.sqrt(sigma2) * rng.standard_normal(x.shape)
+    c = 0.5 / math.sqrt(2.0 * math.pi * sigma2)
+    p0 = c * np.exp(-((y - 1.0) ** 2) / (2.0 * sigma2))
+    p1 = c * np.exp(-((y + 1.0) ** 2) / (2.0 * sigma2))
+    return np.stack([p0, p1], axis=-1), y
+
+
+class LeafRecorder:
+    """Wraps BinaryMemorylessVectorDistribution.calcMarginalizedProbabilities to
+    record the marginal the reference uses at each leaf (xy at information leaves,
+    the a-priori tree at frozen leaves); one call per leaf during decode()."""
+
+    def __init__(self, R):
+        self.cls = R["BMVD"].BinaryMemorylessVectorDistribution
+        self.orig = self.cls.calcMarginalizedProbabilities
+        self.rec = []
+
+    def __enter__(self):
+        rec = self.rec
+        orig = self.orig
+
+        def wrapped(vd):
+            m = orig(vd)
+            rec.append((float(m[0]), float(m[1])))
+            return m
+
+        self.cls.calcMarginalizedProbabilities = wrapped
+        return self
+
+    def __exit__(self, *a):
+        self.cls.calcMarginalizedProbabilities = self.orig
+
+
+def ref_binary_decode_batch(R, N, frozen, crs, xy, prior=None, record_leaves=True):
+    """Decode each codeword of xy [B][N][2] with the reference decoder."""
+    BPED, BMVD = R["BPED"], R["BMVD"]
+    enc = BPED.BinaryPolarEncoderDecoder(N, frozen, crs)
+    xvd = BMVD.BinaryMemorylessVectorDistribution(N)
+    xvd.probs[:] = np.array([0.5, 0.5]) if prior is None else prior
+    B = xy.shape[0]
+    info = np.zeros((B, enc.k), np.uint8)
+    xhat = np.zeros((B, N), np.uint8)
+    leaf = np.zeros((B, N, 2))
+    t0 = time.perf_counter()
+    for b in range(B):
+        xyvd = BMVD.BinaryMemorylessVectorDistribution(N)
+        xyvd.probs[:] = xy[b]
+        with LeafRecorder(R) as lr:
+            (xh, inf) = enc.decode(xvd, xyvd)
+        assert len(lr.rec) == N
+        leaf[b] = np.array(lr.rec)
+        info[b] = inf
+        xhat[b] = xh
+    dt = (time.perf_counter() - t0) / max(B, 1)
+    return enc, info, xhat, leaf, dt
+
+
+def frozen_arrays(enc, N):
+    mask = np.array([1 if i in enc.frozenSet else 0 for i in range(N)], np.uint8)
+    r = np.array(enc.randomlyGeneratedNumbers, np.float64)
+    fval = np.where(0.5 >= r, 0, 1).astype(np.uint8)
+    return mask, r, fval
+
+
+def ref_encode(R, N, enc, info_bits, prior=None):
+    BMVD = R["BMVD"]
+    xvd = BMVD.BinaryMemorylessVectorDistribution(N)
+    xvd.probs[:] = np.array([0.5, 0.5]) if prior is None else prior
+    return np.array(enc.encode(xvd, list(int(v) for v in info_bits)), np.uint8)
+
+
+def save(name, meta, **arrays):
+    os.makedirs(OUT, exist_ok=True)
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, meta=np.array(json.dumps(meta)), **arrays)
+    print("wrote", path, "(%d bytes)" % os.path.getsize(path))
+
+
+# ---------------------------------------------------------------------------
+# fixtures
+# ---------------------------------------------------------------------------
+
+def fx_bsc_n64(R, timing):
+    """C1: N=64, K=32, BSC(0.11); frozen = 32 least reliable by the reference
+    degrading construction (n=6, L=100), ranked by Pe; 1000 codewords."""
+    BMD, BPED = R["BMD"], R["BPED"]
+    n, N, K, L, p = 6, 64, 32, 100, 0.11
+    bsc = BMD.makeBSC(p)
+    dists = [bsc]
+    for _ in range(n):
+        nxt = []
+        for d in dists:
+            nxt.append(d.minusTransform().degrade(L))
+            nxt.append(d.plusTransform().degrade(L))
+        dists = nxt
+    pe = [d.errorProb() for d in dists]
+    order = sorted(range(N), key=lambda k: pe[k])
+    frozen = set(order[K:])
+    crs, irs, chs, T = 1, 1, 1, 1000
+    info_rng = random.Random(irs)
+    chan_rng = random.Random(chs)
+    enc = BPED.BinaryPolarEncoderDecoder(N, frozen, crs)
+    tx_info = np.zeros((T, K), np.uint8)
+    y = np.zeros((T, N), np.uint8)
+    for t in range(T):
+        inf = [0 if info_rng.random() < 0.5 else 1 for _ in range(K)]
+        tx_info[t] = inf
+        x = ref_encode(R, N, enc, inf)
+        for j in range(N):  # test2.py:29-50 channel, with an explicitly seeded RNG
+            rnd = chan_rng.random()
+            s = 0.0
+            for yy in range(2):
+                if s + bsc.probXGivenY(int(x[j]), yy) >= rnd:
+                    y[t, j] = yy
+                    break
+                s += bsc.probXGivenY(int(x[j]), yy)
+    table = np.array(bsc.probs, np.float64)  # [y][x]
+    xy = table[y]
+    enc, info, xhat, leaf, dt = ref_binary_decode_batch(R, N, frozen, crs, xy)
+    mask, r, fval = frozen_arrays(enc, N)
+    errs = int(np.sum(np.any(info != tx_info, axis=1)))
+    timing["bsc_n64_decode_s_per_cw"] = dt
+    save("bsc_n64", dict(config="C1", N=N, K=K, p=p, L=L, crs=crs, info_seed=irs, channel_seed=chs,
+                         construction="reference degrade(L=100) ranked by Pe", frame_errors=errs, trials=T),
+         frozen=mask, r=r, fval=fval, y=y, table=table, tx_info=tx_info, info=info, xhat=xhat, leaf_m=leaf)
+
+
+def fx_awgn(R, timing, n, B, ebn0_db, seed, name, config):
+    BPED = R["BPED"]
+    N, K = 1 << n, 1 << (n - 1)
+    sigma2 = 1.0 / (2.0 * 0.5 * 10 ** (ebn0_db / 10.0))
+    frozen, _ = bhattacharyya_frozen(n, K, sigma2)
+    crs = 7
+    enc = BPED.BinaryPolarEncoderDecoder(N, frozen, crs)
+    rng = np.random.default_rng(seed)
+    tx_info = rng.integers(0, 2, size=(B, K)).astype(np.uint8)
+    x = np.stack([ref_encode(R, N, enc, tx_info[b]) for b in range(B)])
+    xy, _ = awgn_pairs(x, sigma2, rng)
+    enc, info, xhat, leaf, dt = ref_binary_decode_batch(R, N, frozen, crs, xy)
+    mask, r, fval = frozen_arrays(enc, N)
+    errs = int(np.sum(np.any(info != tx_info, axis=1)))
+    timing[name + "_decode_s_per_cw"] = dt
+    save(name, dict(config=config, N=N, K=K, ebn0_db=ebn0_db, sigma2=sigma2, crs=crs, seed=seed,
+                    construction="Bhattacharyya at design Eb/N0", frame_errors=errs, trials=B),
+         frozen=mask, r=r, fval=fval, xy=xy, x=x, tx_info=tx_info, info=info, xhat=xhat, leaf_m=leaf)
+
+
+def fx_edge(R, timing):
+    """Hand-built inputs that exercise the tie / zero / subnormal rules:
+    exact ties (p0 == p1), one-sided zeros (infinite LLR), (0,0) rows,
+    subnormal and huge-ratio rows, at N = 2, 16 and 256."""
+    rng = np.random.default_rng(1234)
+    cases = []
+    for n in (1, 2, 4, 8):
+        N = 1 << n
+        for variant in range(6):
+            B = 24
+            vals = np.array([0.0, 0.5, 0.25, 1.0, 0.125, 1e-300, 4.9e-324, 2.2e-308, 0.3, 0.7, 1e-5])
+            if variant == 0:  # erasure-like: a few discrete levels, many ties and zeros
+                xy = rng.choice(vals[:5], size=(B, N, 2))
+            elif variant == 1:  # subnormal / tiny magnitudes
+                xy = rng.choice(vals, size=(B, N, 2))
+            elif variant == 2:  # random continuous
+                xy = rng.random((B, N, 2))
+            elif variant == 3:  # random with forced one-sided zeros
+                xy = rng.random((B, N, 2))
+                z = rng.random((B, N)) < 0.2
+                side = rng.integers(0, 2, size=(B, N))
+                xy[z, 0] *= side[z]
+                xy[z, 1] *= 1 - side[z]
+            elif variant == 4:  # ties everywhere
+                v = rng.choice(vals[:5], size=(B, N, 1))
+                xy = np.repeat(v, 2, axis=2)
+                flip = rng.random((B, N)) < 0.3
+                xy[flip, 1] = rng.random(int(flip.sum()))
+            else:  # tiny scale: products underflow deep in the tree
+                xy = rng.random((B, N, 2)) * 1e-120
+            frozen = set(int(i) for i in np.nonzero(rng.random(N) < 0.5)[0])
+            crs = int(rng.integers(-1, 50))
+            enc, info, xhat, leaf, dt = ref_binary_decode_batch(R, N, frozen, crs, xy)
+            mask, r, fval = frozen_arrays(enc, N)
+            cases.append(dict(n=n, variant=variant, crs=crs, xy=xy, frozen=mask, r=r, fval=fval,
+                              info=info, xhat=xhat, leaf_m=leaf))
+    arrays = {}
+    for i, c in enumerate(cases):
+        for k, v in c.items():
+            arrays["c%d_%s" % (i, k)] = np.asarray(v)
+    save("edge_binary", dict(cases=len(cases), note="variants: 0 discrete 1 subnormal 2 random 3 one-sided zeros 4 ties 5 underflow"), **arrays)
+
+
+def fx_prior(R, timing):
+    """Non-uniform a-priori distribution: the x-tree decides frozen bits."""
+    rng = np.random.default_rng(77)
+    N, n = 64, 6
+    frozen = set(int(i) for i in rng.permutation(N)[:28])
+    xy = rng.random((40, N, 2))
+    prior = np.array([0.7, 0.3])
+    enc, info, xhat, leaf, dt = ref_binary_decode_batch(R, N, frozen, 11, xy, prior=prior)
+    mask, r, fval = frozen_arrays(enc, N)
+    tx = rng.integers(0, 2, size=(8, enc.k)).astype(np.uint8)
+    xenc = np.stack([ref_encode(R, N, enc, tx[b], prior=prior) for b in range(8)])
+    save("prior_n64", dict(N=N, crs=11, prior=prior.tolist()), frozen=mask, r=r, xy=xy, prior=prior,
+         info=info, xhat=xhat, leaf_m=leaf, enc_info=tx, enc_x=xenc)
+
+
+def fx_encode(R, timing):
+    BPED = R["BPED"]
+    rng = np.random.default_rng(5)
+    out = {}
+    for n in (1, 3, 5, 8, 10):
+        N = 1 << n
+        frozen = set(int(i) for i in np.nonzero(rng.random(N) < 0.4)[0])
+        crs = int(rng.integers(-1, 100))
+        enc = BPED.BinaryPolarEncoderDecoder(N, frozen, crs)
+        B = 16
+        tx = rng.integers(0, 2, size=(B, enc.k)).astype(np.uint8)
+        x = np.stack([ref_encode(R, N, enc, tx[b]) for b in range(B)])
+        u = np.stack([np.array(BPED.polarTransformOfBits([int(v) for v in x[b]]), np.uint8) for b in range(B)])
+        mask, r, fval = frozen_arrays(enc, N)
+        for k, v in dict(frozen=mask, r=r, fval=fval, info=tx, x=x, u=u).items():
+            out["n%d_%s" % (n, k)] = v
+    save("encode_binary", dict(ns=[1, 3, 5, 8, 10]), **out)
+
+
+def fx_qsc(R, timing):
+    """C4: q=4, N=256, QSC(0.11).  Frozen set: the binary Bhattacharyya ranking
+    at z0 = 2*sqrt(p(1-p)) is used as a cheap stand-in (the reference q-ary
+    degrading construction takes ~10 min); parity only needs SOME frozen set."""
+    QPED, QMD = R["QPED"], R["QMD"]
+    q, n, p = 4, 8, 0.11
+    N, K = 1 << n, 128
+    z = np.array([0.6])  # ranking proxy only
+    for _ in range(n):
+        nz = np.empty(2 * len(z))
+        nz[0::2] = np.minimum(1.0, 2 * z - z * z)
+        nz[1::2] = z * z
+        z = nz
+    order = sorted(range(N), key=lambda i: (z[i], i))
+    frozen = set(order[K:])
+    qsc = QMD.makeQSC(q, p)
+    dec = QPED.QaryPolarEncoderDecoder(q, N, frozen, 1)
+    xq = QMD.QaryMemorylessDistribution(q)
+    xq.probs = [qsc.calcXMarginals()]
+    xvd = xq.makeQaryMemorylessVectorDistribution(N, None)
+    rng = random.Random(3)
+    T = 160
+    tx = np.zeros((T, K), np.uint8)
+    y = np.zeros((T, N), np.uint8)
+    xs = np.zeros((T, N), np.uint8)
+    for t in range(T):
+        inf = rng.choices(range(q), k=K)
+        tx[t] = inf
+        x = dec.encode(xvd, inf)
+        xs[t] = x
+        for j in range(N):
+            rnd = rng.random()
+            s = 0.0
+            for yy in range(q):
+                if s + qsc.probXGivenY(int(x[j]), yy) >= rnd:
+                    y[t, j] = yy
+                    break
+                s += qsc.probXGivenY(int(x[j]), yy)
+    table = np.array(qsc.probs, np.float64)
+    info = np.zeros((T, K), np.uint8)
+    t0 = time.perf_counter()
+    for t in range(T):
+        xyvd = qsc.makeQaryMemorylessVectorDistribution(N, [int(v) for v in y[t]])
+        info[t] = dec.decode(xvd, xyvd)
+    timing["qsc_q4_n256_decode_s_per_cw"] = (time.perf_counter() - t0) / T
+    mask = np.array([1 if i in frozen else 0 for i in range(N)], np.uint8)
+    errs = int(np.sum(np.any(info != tx, axis=1)))
+    # extra: random continuous q-ary inputs (not channel-shaped), incl. zeros
+    rs = np.random.default_rng(9)
+    xr = rs.random((24, N, q))
+    xr[rs.random((24, N)) < 0.1] = 0.0
+    xr[:, :, 1][rs.random((24, N)) < 0.2] = 0.0
+    info_r = np.zeros((24, K), np.uint8)
+    for t in range(24):
+        vd = R["QMVD"].QaryMemorylessVectorDistribution(q, N)
+        vd.probs[:] = xr[t]
+        info_r[t] = dec.decode(xvd, vd)
+    save("qsc_q4_n256", dict(config="C4", q=q, N=N, K=K, p=p, seed=3, frame_errors=errs, trials=T,
+                             construction="binary Bhattacharyya stand-in"),
+         frozen=mask, y=y, table=table, tx_info=tx, x=xs, info=info, xy_rand=xr, info_rand=info_r)
+    # q = 3 (non power of two) small case
+    q3, n3 = 3, 5
+    N3 = 1 << n3
+    fr3 = set(int(i) for i in rs.permutation(N3)[:12])
+    dec3 = QPED.QaryPolarEncoderDecoder(q3, N3, fr3, 1)
+    x3 = rs.random((16, N3, q3))
+    x3[rs.random((16, N3)) < 0.1] = 0.0
+    xvd3 = R["QMVD"].QaryMemorylessVectorDistribution(q3, N3)
+    xvd3.probs[:] = 1.0 / 3
+    info3 = np.zeros((16, dec3.k), np.uint8)
+    for t in range(16):
+        vd = R["QMVD"].QaryMemorylessVectorDistribution(q3, N3)
+        vd.probs[:] = x3[t]
+        info3[t] = dec3.decode(xvd3, vd)
+    tx3 = rs.integers(0, q3, size=(8, dec3.k))
+    enc3 = np.stack([np.array(dec3.encode(xvd3, [int(v) for v in tx3[b]]), np.uint8) for b in range(8)])
+    m3 = np.array([1 if i in fr3 else 0 for i in range(N3)], np.uint8)
+    save("qary_q3_n32", dict(q=q3, N=N3), frozen=m3, xy=x3, info=info3, enc_info=tx3.astype(np.uint8), enc_x=enc3)
+
+
+FIXTURES = {
+    "bsc_n64": fx_bsc_n64,
+    "awgn_n1024": lambda R, t: fx_awgn(R, t, 10, 64, 2.0, 20250204, "awgn_n1024", "C2"),
+    "awgn_n4096": lambda R, t: fx_awgn(R, t, 12, 12, 2.0, 4096, "awgn_n4096", "C3"),
+    "awgn_n256_lowsnr": lambda R, t: fx_awgn(R, t, 8, 64, 0.0, 256, "awgn_n256_lowsnr", "low-SNR"),
+    "edge_binary": fx_edge,
+    "prior_n64": fx_prior,
+    "encode_binary": fx_encode,
+    "qsc_q4_n256": fx_qsc,
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*")
+    args = ap.parse_args()
+    R = load_reference()
+    tpath = os.path.join(OUT, "ref_timing.json")
+    timing = json.load(open(tpath)) if os.path.exists(tpath) else {}
+    for name, fn in FIXTURES.items():
+        if args.only and name not in args.only:
+            continue
+        t0 = time.time()
+        fn(R, timing)
+        print("  %s: %.1f s" % (name, time.time() - t0))
+    timing["host"] = "build container, 1 thread, shimmed reference Python (decode only)"
+    os.makedirs(OUT, exist_ok=True)
+    with open(tpath, "w") as f:
+        json.dump(timing, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,88 @@
+/*
+ * polarcub_sc.h -- C ABI of the MI355X (gfx950) polar SC hot path.
+ *
+ * This is the drop-in boundary for the reference's decode path.  The
+ * reference (benjilieber/polarcub) is pure Python; the functions below are
+ * what its per-codeword calls become when batched:
+ *
+ *   pcub_sc_decode_bin   replaces BinaryPolarEncoderDecoder.decode
+ *                        (BinaryPolarEncoderDecoder.py:71-99) and the recursion it
+ *                        drives (:223-325) over BinaryMemorylessVectorDistribution
+ *                        (VectorDistributions/BinaryMemorylessVectorDistribution.py:15-87),
+ *                        for a uniform a-priori distribution.
+ *   pcub_sc_decode_qary  replaces QaryPolarEncoderDecoder.decode
+ *                        (QaryPolarEncoderDecoder.py:90-116, :318-401) over
+ *                        QaryMemorylessVectorDistribution (:26-118).
+ *   pcub_polar_encode_bin replaces BinaryPolarEncoderDecoder.encode
+ *                        (BinaryPolarEncoderDecoder.py:46-69) for a uniform prior.
+ *   pcub_pack_bits / pcub_unpack_bits / pcub_transpose_pairs: layout helpers.
+ *
+ * Conventions
+ *   - All data pointers are DEVICE pointers (hipMalloc'd or torch CUDA tensors).
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream); every
+ *     call is stream-ordered and asynchronous; no call synchronises or allocates.
+ *   - Bit vectors are "word-major, codeword-minor": word w of codeword b is at
+ *     words[w * B + b] (32 bits per word, bit t = element 32w+t).  This is the
+ *     coalesced layout for one-codeword-per-lane kernels.
+ *   - Joint probabilities use the "element-major" layout: xy[(i * B + b) * 2 + x]
+ *     = P(X_i = x, Y_i = y_i) of codeword b (binary), i.e. a [N][B][2] array.
+ *     pcub_transpose_pairs converts from the reference's per-codeword [B][N][2].
+ *   - Return value: 0 on success, PCUB_EINVAL (-1) for invalid arguments,
+ *     otherwise the hipError_t of the failed launch.
+ *   - Arithmetic contract: IEEE binary64 in the reference's operation order;
+ *     decisions are bit-identical to the reference for finite, non-negative
+ *     inputs (zeros, subnormals and exact ties included).
+ */
+#ifndef POLARCUB_SC_H
+#define POLARCUB_SC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCUB_EINVAL (-1)
+
+/* Library version, for the loader's ABI check. */
+int pcub_abi_version(void);
+
+/* Bytes of device workspace pcub_sc_decode_bin needs for a batch of B
+ * codewords of length 2^log2N (0 for invalid arguments).  The workspace holds
+ * the per-slot SC stage buffers; it is sized by the resident grid, not by B. */
+size_t pcub_sc_decode_bin_workspace(int64_t B, int32_t log2N);
+
+/* Binary SC decode of B codewords, uniform a-priori distribution.
+ *   xy          [N][B][2] f64 joint probabilities (never modified)
+ *   frozen_mask ceil(N/32) u32 words, bit i set <=> u_i frozen
+ *   frozen_val  ceil(N/32) u32 words, value of each frozen u_i
+ *               (reference: 0 if 0.5 >= r_i else 1, BinaryPolarEncoderDecoder.py:258-262)
+ *   K           number of information positions (N - popcount(frozen_mask))
+ *   info_words  out, ceil(K/32) x B words: decoded information bits in u order
+ *   xhat_words  out, ceil(N/32) x B words: re-encoded codeword estimate (may be NULL)
+ *   u_words     out, ceil(N/32) x B words: all N decisions u_0..u_{N-1} (may be NULL)
+ *   workspace   device buffer of pcub_sc_decode_bin_workspace(B, log2N) bytes */
+int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                       const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
+                       uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Polar encoder (uniform prior): u_i = frozen_val_i at frozen positions, the
+ * next information bit elsewhere; x = polar transform of u in the reference's
+ * adjacent-pair convention (BinaryPolarEncoderDecoder.py:319-323, :494-516).
+ *   info_words ceil(K/32) x B, x_words out ceil(N/32) x B. */
+int pcub_polar_encode_bin(const uint32_t* info_words, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                          const uint32_t* frozen_val, int32_t K, uint32_t* x_words, void* stream);
+
+/* [B][nbits] u8 (0/1) -> ceil(nbits/32) x B words, and back. */
+int pcub_pack_bits(const uint8_t* bits, int64_t B, int32_t nbits, uint32_t* words, void* stream);
+int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits, uint8_t* bits, void* stream);
+
+/* [B][N][q] f64 -> [N][B][q] f64 (q = 2 for binary pairs). */
+int pcub_transpose_pairs(const double* src, int64_t B, int32_t N, int32_t q, double* dst, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* POLARCUB_SC_H */

@@ -1,0 +1,65 @@
+"""ctypes binding of the HIP C-ABI library (include/polarcub_sc.h).
+
+There is no CPU fallback: if the library is missing or a call fails, this
+module raises.  Device pointers come from torch CUDA (HIP) tensors.
+"""
+import ctypes
+import os
+
+from . import build as _build
+
+_c_void_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+
+_lib = None
+
+EINVAL = -1
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpolarcub_hip.so (building it in-tree first if it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if not os.path.exists(path):
+        _build.build()
+    L = ctypes.CDLL(path)
+    L.pcub_abi_version.restype = ctypes.c_int
+    L.pcub_abi_version.argtypes = []
+    L.pcub_sc_set_variant.restype = ctypes.c_int
+    L.pcub_sc_set_variant.argtypes = [ctypes.c_int]
+    L.pcub_sc_decode_bin_workspace.restype = ctypes.c_size_t
+    L.pcub_sc_decode_bin_workspace.argtypes = [_i64, _i32]
+    L.pcub_sc_decode_bin.restype = ctypes.c_int
+    L.pcub_sc_decode_bin.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                                     _c_void_p, _c_void_p, ctypes.c_size_t, _c_void_p]
+    L.pcub_polar_encode_bin.restype = ctypes.c_int
+    L.pcub_polar_encode_bin.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p]
+    L.pcub_pack_bits.restype = ctypes.c_int
+    L.pcub_pack_bits.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p]
+    L.pcub_unpack_bits.restype = ctypes.c_int
+    L.pcub_unpack_bits.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p]
+    L.pcub_transpose_pairs.restype = ctypes.c_int
+    L.pcub_transpose_pairs.argtypes = [_c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p]
+    if L.pcub_abi_version() != 1:
+        raise ImportError("libpolarcub_hip.so ABI mismatch; rebuild with python -m polarcub_amd.build --force")
+    _lib = L
+    return L
+
+
+# every exported symbol declared in include/polarcub_sc.h
+EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_bin", "pcub_polar_encode_bin",
+           "pcub_pack_bits", "pcub_unpack_bits", "pcub_transpose_pairs"]
+
+
+def check(rc, what):
+    if rc != 0:
+        if rc == EINVAL:
+            raise ValueError("%s: invalid arguments (PCUB_EINVAL)" % what)
+        raise HipError("%s failed: hipError_t %d" % (what, rc))

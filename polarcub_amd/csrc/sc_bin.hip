@@ -1,0 +1,164 @@
+// sc_bin.hip -- binary SC decode kernels for gfx950 + their C-ABI launchers.
+//
+// pcub_sc_decode_bin replaces BinaryPolarEncoderDecoder.decode
+// (BinaryPolarEncoderDecoder.py:71-99) for a batch of codewords with a uniform
+// a-priori distribution.  The schedule is in sc_bin_body.h; this file owns the
+// launch geometry:
+//   * 256-thread workgroups, one codeword per lane;
+//   * a resident ("persistent") grid of CUs x occupancy workgroups that
+//     strides over 256-codeword tiles, so the per-slot stage buffers are reused
+//     and stay warm in L2 / Infinity Cache instead of being re-allocated per
+//     codeword;
+//   * padding lanes of the last tile decode a duplicate codeword and store
+//     nothing, so every wave runs the same schedule.
+#include <hip/hip_runtime.h>
+
+#include "polarcub_sc.h"
+#include "sc_bin_body.h"
+
+using namespace pcub;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// Variants: register-subtree length S and the minimum waves/SIMD the register
+// allocation must allow (launch-bounds).  Variant 0 is the default.
+//   0: S = 16, 2 waves/SIMD (219 VGPRs)     1: S = 8, 4 waves/SIMD (124 VGPRs)
+constexpr int kNumVariants = 2;
+constexpr int kVarS[kNumVariants] = {16, 8};
+
+template <int S, int W>
+__global__ __launch_bounds__(kBlock, W) void k_sc_bin(BinArgs A) {
+    const long long slot = (long long)blockIdx.x * kBlock + threadIdx.x;
+    const long long ntiles = (A.B + kBlock - 1) / kBlock;
+    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const long long cw = t * kBlock + threadIdx.x;
+        const bool valid = cw < A.B;
+        decode_codeword<S>(A, valid ? cw : A.B - 1, slot, valid);
+    }
+}
+
+template <int NN>
+__global__ __launch_bounds__(kBlock) void k_sc_bin_small(BinArgs A) {
+    const long long cw = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (cw < A.B) decode_small<NN>(A, cw, true);
+}
+
+typedef void (*KernFn)(BinArgs);
+KernFn variant_kernel(int v) {
+    return v == 1 ? k_sc_bin<8, 4> : k_sc_bin<16, 2>;
+}
+
+int g_variant = 0;
+
+struct DevInfo {
+    int dev = -1;
+    int cus = 0;
+    int occ[kNumVariants] = {0, 0};
+};
+
+DevInfo dev_info() {
+    static thread_local DevInfo cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return DevInfo{};
+    if (cache.dev == dev) return cache;
+    DevInfo d;
+    d.dev = dev;
+    if (hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return DevInfo{};
+    for (int v = 0; v < kNumVariants; ++v) {
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, variant_kernel(v), kBlock, 0) != hipSuccess || occ < 1)
+            occ = 1;
+        d.occ[v] = occ;
+    }
+    cache = d;
+    return d;
+}
+
+size_t slot_bytes(int n, int S) {
+    const size_t N = (size_t)1 << n;
+    return (N / 2 - S) * sizeof(double2) + (N / 32) * sizeof(uint32_t);
+}
+
+long long grid_for(long long B, int v) {
+    const DevInfo d = dev_info();
+    if (d.cus <= 0) return 0;
+    const long long ntiles = (B + kBlock - 1) / kBlock;
+    long long g = (long long)d.cus * d.occ[v];
+    return ntiles < g ? ntiles : g;
+}
+
+// the subtree must leave at least one outer level: N >= 2S
+int pick_variant(int n) {
+    int v = g_variant;
+    if ((1 << n) < 2 * kVarS[v]) v = 1;
+    return v;
+}
+
+}  // namespace
+
+extern "C" int pcub_abi_version(void) { return 1; }
+
+// Tuning hook (not part of the stable ABI): choose the decode kernel variant.
+extern "C" int pcub_sc_set_variant(int v) {
+    if (v < 0 || v >= kNumVariants) return PCUB_EINVAL;
+    g_variant = v;
+    return 0;
+}
+
+extern "C" size_t pcub_sc_decode_bin_workspace(int64_t B, int32_t log2N) {
+    if (B <= 0 || log2N < 0 || log2N > 24) return 0;
+    if (log2N < 6) return 0;
+    const int v = pick_variant(log2N);
+    const long long g = grid_for(B, v);
+    return (size_t)g * kBlock * slot_bytes(log2N, kVarS[v]);
+}
+
+extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                                  const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
+                                  uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream) {
+    if (B < 0 || log2N < 0 || log2N > 24 || !frozen_mask || !frozen_val) return PCUB_EINVAL;
+    if (K < 0 || K > (1 << log2N) || (K > 0 && !info_words) || (B > 0 && !xy)) return PCUB_EINVAL;
+    if (B == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    BinArgs A;
+    A.xy = (const double2*)xy;
+    A.B = B;
+    A.n = log2N;
+    A.fmask = frozen_mask;
+    A.fval = frozen_val;
+    A.info = info_words;
+    A.xhat = xhat_words;
+    A.uout = u_words;
+    A.scratch = nullptr;
+    A.ybits = nullptr;
+    A.nslots = 0;
+    if (log2N <= 5) {
+        const dim3 grid((unsigned)((B + kBlock - 1) / kBlock));
+        switch (log2N) {
+            case 0: hipLaunchKernelGGL(k_sc_bin_small<1>, grid, dim3(kBlock), 0, st, A); break;
+            case 1: hipLaunchKernelGGL(k_sc_bin_small<2>, grid, dim3(kBlock), 0, st, A); break;
+            case 2: hipLaunchKernelGGL(k_sc_bin_small<4>, grid, dim3(kBlock), 0, st, A); break;
+            case 3: hipLaunchKernelGGL(k_sc_bin_small<8>, grid, dim3(kBlock), 0, st, A); break;
+            case 4: hipLaunchKernelGGL(k_sc_bin_small<16>, grid, dim3(kBlock), 0, st, A); break;
+            default: hipLaunchKernelGGL(k_sc_bin_small<32>, grid, dim3(kBlock), 0, st, A); break;
+        }
+        return (int)hipGetLastError();
+    }
+    const int v = pick_variant(log2N);
+    const int S = kVarS[v];
+    long long g = grid_for(B, v);
+    if (g <= 0) return (int)hipErrorNoDevice;
+    const size_t per_block = (size_t)kBlock * slot_bytes(log2N, S);
+    if (!workspace) return PCUB_EINVAL;
+    if ((size_t)g * per_block > workspace_bytes) g = (long long)(workspace_bytes / per_block);
+    if (g <= 0) return PCUB_EINVAL;
+    const long long nslots = g * kBlock;
+    const size_t N = (size_t)1 << log2N;
+    A.nslots = nslots;
+    A.scratch = (double2*)workspace;
+    A.ybits = (uint32_t*)((char*)workspace + (size_t)nslots * (N / 2 - S) * sizeof(double2));
+    hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), 0, st, A);
+    return (int)hipGetLastError();
+}

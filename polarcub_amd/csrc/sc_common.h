@@ -1,0 +1,190 @@
+// sc_common.h -- device-side arithmetic shared by the SC kernels (gfx950).
+//
+// Value representation ("compact normalised pair").  After every minus/plus
+// transform the reference max-normalises each pair
+// (VectorDistributions/BinaryMemorylessVectorDistribution.py:71-87):
+//     t = max(p0, p1); if t == 0: t = 1; p0 /= t; p1 /= t
+// so a normalised pair is exactly (1, r), (r, 1) with r = min/max in [0,1], or
+// (0, 0).  We store it in ONE binary64:
+//     +r   <=> (1, r)
+//     -r   <=> (r, 1)        (-0.0 encodes (0, 1); the tie (1,1) may carry either sign)
+//     2.0  <=> (0, 0)        ("sentinel", any value > 1)
+// x/x == 1 exactly for finite non-zero x, so the stored form loses nothing.
+//
+// Canonical arithmetic.  Swapping the two components of an input flips the
+// output of the minus transform (its two sums are the same rounded terms,
+// commuted), and flips the plus transform's output when both inputs flip.
+// Hence each transform is evaluated on the canonical forms (1, ra), (1, rb)
+// and the orientation is tracked with an XOR; every formula below is an exact
+// restatement of the reference's rounded operations for the actual pair (see
+// DESIGN.md, "Arithmetic contract").  Division is the compiler's IEEE
+// correctly-rounded f64 sequence; the library is built with -ffp-contract=off.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PCUB_HD __host__ __device__ __forceinline__
+
+namespace pcub {
+
+constexpr double kSentinel = 2.0;
+
+PCUB_HD long long as_bits(double v) { return __builtin_bit_cast(long long, v); }
+PCUB_HD double from_bits(long long b) { return __builtin_bit_cast(double, b); }
+
+struct CV {
+    double r;    // ratio in [0,1] (garbage when z)
+    uint32_t s;  // orientation: 1 <=> (r, 1)
+    bool z;      // (0, 0)
+};
+
+PCUB_HD CV cv_load(double v) {
+    CV c;
+    c.s = (uint32_t)((unsigned long long)as_bits(v) >> 63);
+    c.r = __builtin_fabs(v);
+    c.z = c.r > 1.0;
+    return c;
+}
+
+PCUB_HD double cv_pack(double q, uint32_t s, bool z) {
+    // q >= +0 always, so OR-ing the sign bit in is exact negation.
+    double o = from_bits(as_bits(q) | (long long)((unsigned long long)s << 63));
+    return z ? kSentinel : o;
+}
+
+// max-normalise an un-normalised pair (p0, p1 >= 0) into compact form.
+PCUB_HD double norm_pack(double p0, double p1) {
+    const bool sw = p1 > p0;
+    const double num = sw ? p0 : p1;
+    const double den = sw ? p1 : p0;
+    const bool z = den == 0.0;  // max == 0 => both zero
+    const double q = num / (z ? 1.0 : den);
+    return cv_pack(q, sw ? 1u : 0u, z);
+}
+
+// minus transform (BinaryMemorylessVectorDistribution.py:15-29) + normalise,
+// on compact inputs a = row 2h, b = row 2h+1.
+//   canonical:  p0 = 1*1 + ra*rb,  p1 = 1*rb + ra*1
+PCUB_HD double op_f(double va, double vb) {
+    const CV a = cv_load(va), b = cv_load(vb);
+    const double m = a.r * b.r;
+    const double p0 = 1.0 + m;
+    const double p1 = a.r + b.r;
+    const bool sw = p1 > p0;
+    const double num = sw ? p0 : p1;
+    const double den = sw ? p1 : p0;  // >= 1 unless an input is the sentinel
+    const double q = num / den;
+    return cv_pack(q, a.s ^ b.s ^ (sw ? 1u : 0u), a.z | b.z);
+}
+
+// plus transform (BinaryMemorylessVectorDistribution.py:31-47) + normalise.
+// u == 1 swaps a's components.  Same orientation: (1*1, ra*rb) -> (1, ra*rb),
+// no division.  Opposite orientation: the pair is (ra, rb) or (rb, ra), whose
+// normalised ratio is min/max.
+PCUB_HD double op_g(double va, double vb, uint32_t u) {
+    const CV a = cv_load(va), b = cv_load(vb);
+    bool z = a.z | b.z;
+    double q;
+    uint32_t s;
+    if ((a.s ^ u) == b.s) {
+        q = a.r * b.r;
+        s = b.s;
+    } else {
+        const double mx = a.r > b.r ? a.r : b.r;
+        const double mn = a.r > b.r ? b.r : a.r;
+        s = b.s ? (a.r > b.r ? 1u : 0u) : (b.r > a.r ? 1u : 0u);
+        z = z | (mx == 0.0);
+        q = mn / (mx == 0.0 ? 1.0 : mx);
+    }
+    return cv_pack(q, s, z);
+}
+
+// raw (un-normalised) root rows: the root is never normalised by the reference.
+PCUB_HD double op_f_raw(double2 a, double2 b) {
+    const double p0 = a.x * b.x + a.y * b.y;
+    const double p1 = a.x * b.y + a.y * b.x;
+    return norm_pack(p0, p1);
+}
+
+PCUB_HD double op_g_raw(double2 a, double2 b, uint32_t u) {
+    const double p0 = u ? a.y * b.x : a.x * b.x;
+    const double p1 = u ? a.x * b.y : a.y * b.y;
+    return norm_pack(p0, p1);
+}
+
+// Leaf decisions.  The reference normalises the leaf, takes m = p / (p0 + p1)
+// and decides 0 iff m0 >= m1 (BinaryPolarEncoderDecoder.py:250-252).  For a
+// normalised (1, r) that is always 0; for (r, 1) with r < 1 it is always 1
+// (r/s < 1/2 <= 1/s with s = fl(1 + r)); (0,0) gives 0.  So the
+// decision is "p1 > p0" of the un-normalised transform output.
+PCUB_HD uint32_t leaf_f(double va, double vb) {
+    const CV a = cv_load(va), b = cv_load(vb);
+    const double m = a.r * b.r;
+    const double p0 = 1.0 + m;
+    const double p1 = a.r + b.r;
+    const bool d = (a.s ^ b.s) ? (p0 > p1) : (p1 > p0);
+    return (d && !(a.z | b.z)) ? 1u : 0u;
+}
+
+PCUB_HD uint32_t leaf_g(double va, double vb, uint32_t u) {
+    const CV a = cv_load(va), b = cv_load(vb);
+    bool d;
+    if ((a.s ^ u) == b.s) {
+        d = b.s && (a.r * b.r < 1.0);
+    } else {
+        // actual pair (x0, x1) = b.s ? (rb, ra) : (ra, rb)
+        d = b.s ? (a.r > b.r) : (b.r > a.r);
+    }
+    return (d && !(a.z | b.z)) ? 1u : 0u;
+}
+
+// single leaf from a compact value: 1 <=> (r, 1) with r < 1.  (A tie (1,1) may
+// be stored as +1.0 or -1.0; both decide 0.)
+PCUB_HD uint32_t leaf_v(double v) {
+    const CV a = cv_load(v);
+    return (a.s && !a.z && a.r < 1.0) ? 1u : 0u;
+}
+
+PCUB_HD uint32_t bitrev(uint32_t x, int nbits) {
+    return nbits == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - nbits));
+}
+
+// Register-resident subtree of length L (compile-time), half-split storage:
+// children are f/g of (v[j], v[j + L/2]); the encoding of the node is
+// [ym ^ yp | yp] (bit j of the result = encoded bit at half-split position j).
+// u decisions for leaf BASE+i are OR-ed into ub bit BASE+i.
+template <int L, int BASE>
+struct Sub {
+    static PCUB_HD uint32_t run(const double* v, uint32_t& ub, uint32_t fm, uint32_t fv) {
+        double c[L / 2];
+#pragma unroll
+        for (int j = 0; j < L / 2; ++j) c[j] = op_f(v[j], v[j + L / 2]);
+        const uint32_t ym = Sub<L / 2, BASE>::run(c, ub, fm, fv);
+#pragma unroll
+        for (int j = 0; j < L / 2; ++j) c[j] = op_g(v[j], v[j + L / 2], (ym >> j) & 1u);
+        const uint32_t yp = Sub<L / 2, BASE + L / 2>::run(c, ub, fm, fv);
+        return (ym ^ yp) | (yp << (L / 2));
+    }
+};
+
+template <int BASE>
+struct Sub<2, BASE> {
+    static PCUB_HD uint32_t run(const double* v, uint32_t& ub, uint32_t fm, uint32_t fv) {
+        const uint32_t fz0 = (fm >> BASE) & 1u, fz1 = (fm >> (BASE + 1)) & 1u;
+        const uint32_t u0 = fz0 ? ((fv >> BASE) & 1u) : leaf_f(v[0], v[1]);
+        const uint32_t u1 = fz1 ? ((fv >> (BASE + 1)) & 1u) : leaf_g(v[0], v[1], u0);
+        ub |= (u0 << BASE) | (u1 << (BASE + 1));
+        return (u0 ^ u1) | (u1 << 1);
+    }
+};
+
+template <int BASE>
+struct Sub<1, BASE> {
+    static PCUB_HD uint32_t run(const double* v, uint32_t& ub, uint32_t fm, uint32_t fv) {
+        const uint32_t u0 = ((fm >> BASE) & 1u) ? ((fv >> BASE) & 1u) : leaf_v(v[0]);
+        ub |= u0 << BASE;
+        return u0;
+    }
+};
+
+}  // namespace pcub

@@ -1,0 +1,155 @@
+// sc_util.hip -- polar encoder and layout kernels (gfx950) + C-ABI launchers.
+//
+// pcub_polar_encode_bin replaces BinaryPolarEncoderDecoder.encode
+// (BinaryPolarEncoderDecoder.py:46-69) under a uniform prior, where the a-priori
+// tree is constant and every frozen bit is the precomputed 0.5 >= r_i test
+// (:258-262).  With u in natural order, the reference's adjacent-pair combine
+// (:319-323) equals x = bitrev_N(F u), F u evaluated in place as
+//     for h = 1, 2, 4, .., N/2: every block of 2h: left half ^= right half
+// (32-bit words: h < 32 inside a word by shift/mask, h >= 32 word-wise).
+#include <hip/hip_runtime.h>
+
+#include "polarcub_sc.h"
+#include "sc_common.h"
+
+using namespace pcub;
+
+namespace {
+
+constexpr int kEncBlock = 64;
+
+__global__ __launch_bounds__(kEncBlock) void k_encode_bin(const uint32_t* __restrict__ info, long long B, int n,
+                                                          const uint32_t* __restrict__ fmask,
+                                                          const uint32_t* __restrict__ fval, int K,
+                                                          uint32_t* __restrict__ x) {
+    extern __shared__ uint32_t sm[];  // [W][kEncBlock]
+    const int N = 1 << n;
+    const int W = N >= 32 ? N / 32 : 1;
+    const int lane = threadIdx.x;
+    const long long cw = (long long)blockIdx.x * kEncBlock + lane;
+    const bool valid = cw < B;
+    const long long cwl = valid ? cw : B - 1;
+    uint32_t* u = sm + lane;
+    // 1) u in natural order, in-word butterflies
+    int iw = 0, ileft = 0;
+    uint32_t ibuf = 0;
+    const uint32_t lastmask = N >= 32 ? 0xffffffffu : ((1u << N) - 1u);
+    for (int w = 0; w < W; ++w) {
+        const uint32_t fm = fmask[w], fv = fval[w];
+        uint32_t uw = fv & fm & lastmask;
+        for (uint32_t m = ~fm & lastmask; m != 0u; m &= m - 1u) {
+            if (ileft == 0) {
+                ibuf = info[(long long)iw * B + cwl];
+                ++iw;
+                ileft = 32;
+            }
+            uw |= (ibuf & 1u) << __builtin_ctz(m);
+            ibuf >>= 1;
+            --ileft;
+        }
+        uw ^= (uw >> 1) & 0x55555555u;
+        uw ^= (uw >> 2) & 0x33333333u;
+        uw ^= (uw >> 4) & 0x0f0f0f0fu;
+        uw ^= (uw >> 8) & 0x00ff00ffu;
+        uw ^= (uw >> 16) & 0x0000ffffu;
+        u[w * kEncBlock] = uw;
+    }
+    // 2) word-level butterflies
+    for (int hw = 1; hw < W; hw <<= 1)
+        for (int b0 = 0; b0 < W; b0 += 2 * hw)
+            for (int i = 0; i < hw; ++i) u[(b0 + i) * kEncBlock] ^= u[(b0 + hw + i) * kEncBlock];
+    // 3) x = bitrev_N(F u)
+    if (!valid) return;
+    const int tb = N >= 32 ? 32 : N;
+    for (int w = 0; w < W; ++w) {
+        uint32_t o = 0;
+        for (int t = 0; t < tb; ++t) {
+            const uint32_t p = bitrev((uint32_t)(32 * w + t), n);
+            o |= ((u[(p >> 5) * kEncBlock] >> (p & 31u)) & 1u) << t;
+        }
+        x[(long long)w * B + cw] = o;
+    }
+}
+
+__global__ void k_pack_bits(const uint8_t* __restrict__ bits, long long B, int nbits, uint32_t* __restrict__ words) {
+    const int W = (nbits + 31) / 32;
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)W * B) return;
+    const long long b = idx % B;
+    const int w = (int)(idx / B);
+    uint32_t o = 0;
+    for (int t = 0; t < 32; ++t) {
+        const int i = 32 * w + t;
+        if (i < nbits) o |= (uint32_t)(bits[b * nbits + i] & 1u) << t;
+    }
+    words[idx] = o;
+}
+
+__global__ void k_unpack_bits(const uint32_t* __restrict__ words, long long B, int nbits, uint8_t* __restrict__ bits) {
+    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long long)nbits * B) return;
+    const long long b = idx / nbits;
+    const int i = (int)(idx % nbits);
+    bits[idx] = (uint8_t)((words[(long long)(i >> 5) * B + b] >> (i & 31)) & 1u);
+}
+
+// [B][N][q] -> [N][B][q] through a 32x32-element LDS tile.
+__global__ void k_transpose(const double* __restrict__ src, long long B, int N, int q, double* __restrict__ dst) {
+    __shared__ double tile[32][33 * 4];
+    const long long b0 = (long long)blockIdx.x * 32;
+    const int i0 = blockIdx.y * 32;
+    const int tx = threadIdx.x, ty = threadIdx.y;  // 32 x 8
+    for (int r = ty; r < 32; r += 8) {
+        const long long b = b0 + r;
+        const int i = i0 + tx;
+        if (b < B && i < N)
+            for (int c = 0; c < q; ++c) tile[r][tx * q + c] = src[(b * N + i) * q + c];
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const int i = i0 + r;
+        const long long b = b0 + tx;
+        if (b < B && i < N)
+            for (int c = 0; c < q; ++c) dst[((long long)i * B + b) * q + c] = tile[tx][r * q + c];
+    }
+}
+
+}  // namespace
+
+extern "C" int pcub_polar_encode_bin(const uint32_t* info_words, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                                     const uint32_t* frozen_val, int32_t K, uint32_t* x_words, void* stream) {
+    if (B < 0 || log2N < 0 || log2N > 14 || !frozen_mask || !frozen_val || !x_words) return PCUB_EINVAL;
+    if (K < 0 || K > (1 << log2N) || (K > 0 && !info_words)) return PCUB_EINVAL;
+    if (B == 0) return 0;
+    const int W = log2N >= 5 ? (1 << (log2N - 5)) : 1;
+    const size_t lds = (size_t)W * kEncBlock * sizeof(uint32_t);
+    hipLaunchKernelGGL(k_encode_bin, dim3((unsigned)((B + kEncBlock - 1) / kEncBlock)), dim3(kEncBlock), lds,
+                       (hipStream_t)stream, info_words, (long long)B, log2N, frozen_mask, frozen_val, K, x_words);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcub_pack_bits(const uint8_t* bits, int64_t B, int32_t nbits, uint32_t* words, void* stream) {
+    if (B < 0 || nbits < 0 || (B > 0 && nbits > 0 && (!bits || !words))) return PCUB_EINVAL;
+    const long long total = (long long)((nbits + 31) / 32) * B;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, bits,
+                       (long long)B, nbits, words);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits, uint8_t* bits, void* stream) {
+    if (B < 0 || nbits < 0 || (B > 0 && nbits > 0 && (!bits || !words))) return PCUB_EINVAL;
+    const long long total = (long long)nbits * B;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(k_unpack_bits, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, words,
+                       (long long)B, nbits, bits);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcub_transpose_pairs(const double* src, int64_t B, int32_t N, int32_t q, double* dst, void* stream) {
+    if (B < 0 || N < 0 || q < 1 || q > 4 || (B > 0 && N > 0 && (!src || !dst))) return PCUB_EINVAL;
+    if (B == 0 || N == 0) return 0;
+    const dim3 grid((unsigned)((B + 31) / 32), (unsigned)((N + 31) / 32));
+    hipLaunchKernelGGL(k_transpose, grid, dim3(32, 8), 0, (hipStream_t)stream, src, (long long)B, N, q, dst);
+    return (int)hipGetLastError();
+}

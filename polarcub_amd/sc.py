@@ -1,0 +1,205 @@
+"""Batched binary SC decode / encode on MI355X through the HIP C-ABI.
+
+This is the batch entry point underneath the reference-compatible facade
+(polarcub_amd.coding.BinaryPolarEncoderDecoder).  Tensors are torch CUDA (HIP)
+tensors; every call is asynchronous on torch's current stream.
+
+Layouts (see include/polarcub_sc.h):
+  * joint probabilities, native:  [N, B, 2] float64  (element-major, codeword-minor)
+  * joint probabilities, per-cw:  [B, N, 2] float64  (the reference's probs[i][x], stacked)
+  * bit vectors, packed:          [ceil(nbits/32), B] int32 words (bit t of word w = bit 32w+t)
+  * bit vectors, unpacked:        [B, nbits] uint8
+"""
+import ctypes
+import random
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _log2(N):
+    n = int(N).bit_length() - 1
+    if N < 1 or (1 << n) != N:
+        raise ValueError("code length must be a power of two, got %r" % (N,))
+    return n
+
+
+def pack_rows(bits):
+    """Host helper: [B, nbits] 0/1 -> [ceil(nbits/32), B] uint32 (numpy)."""
+    bits = np.asarray(bits, dtype=np.uint8)
+    if bits.ndim == 1:
+        bits = bits[None, :]
+    B, nb = bits.shape
+    W = max(1, (nb + 31) // 32)
+    pad = np.zeros((B, W * 32), np.uint64)
+    pad[:, :nb] = bits & 1
+    words = (pad.reshape(B, W, 32) << np.arange(32, dtype=np.uint64)).sum(-1).astype(np.uint32)
+    return np.ascontiguousarray(words.T)
+
+
+def unpack_rows(words, nbits):
+    """Host helper: [W, B] uint32 words -> [B, nbits] uint8."""
+    words = np.asarray(words).view(np.uint32) if np.asarray(words).dtype == np.int32 else np.asarray(words, np.uint32)
+    W, B = words.shape
+    b = ((words.T[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).astype(np.uint8).reshape(B, W * 32)
+    return b[:, :nbits]
+
+
+def common_randomness(N, seed):
+    """r_i of BinaryPolarEncoderDecoder.initializeFrozenOrInformationAndRandomlyGeneratedNumbers
+    (BinaryPolarEncoderDecoder.py:33-44): MT19937 draws for every index, or 1.0 for seed -1."""
+    if seed == -1:
+        return np.ones(N)
+    rng = random.Random()
+    rng.seed(seed)
+    return np.array([rng.random() for _ in range(N)])
+
+
+class CodeSpec:
+    """One binary polar code: length, frozen positions and frozen values, resident on the device.
+
+    frozen_values follow the reference's uniform-prior rule u_i = 0 if 0.5 >= r_i else 1
+    (BinaryPolarEncoderDecoder.py:258-262); use from_frozen_set() to derive them from
+    commonRandomnessSeed exactly as the reference does.
+    """
+
+    def __init__(self, N, frozen_mask, frozen_values=None, device=None):
+        self.N = int(N)
+        self.n = _log2(self.N)
+        mask = np.asarray(frozen_mask, dtype=np.uint8).reshape(-1)
+        if mask.shape[0] != self.N:
+            raise ValueError("frozen mask has %d entries, expected N=%d" % (mask.shape[0], self.N))
+        mask = (mask != 0).astype(np.uint8)
+        vals = np.zeros(self.N, np.uint8) if frozen_values is None else (np.asarray(frozen_values) != 0).astype(np.uint8)
+        vals = vals & mask
+        self.frozen_mask = mask
+        self.frozen_values = vals
+        self.K = int(self.N - int(mask.sum()))
+        self.device = torch.device("cuda") if device is None else torch.device(device)
+        self.fmask_dev = torch.from_numpy(pack_rows(mask).reshape(-1).view(np.int32).copy()).to(self.device)
+        self.fval_dev = torch.from_numpy(pack_rows(vals).reshape(-1).view(np.int32).copy()).to(self.device)
+
+    @classmethod
+    def from_frozen_set(cls, N, frozen_set, common_randomness_seed, device=None):
+        mask = np.zeros(int(N), np.uint8)
+        for i in frozen_set:
+            mask[int(i)] = 1
+        r = common_randomness(int(N), common_randomness_seed)
+        vals = np.where(0.5 >= r, 0, 1).astype(np.uint8)
+        return cls(N, mask, vals, device=device)
+
+    @property
+    def info_words(self):
+        return (self.K + 31) // 32
+
+    @property
+    def n_words(self):
+        return max(1, (self.N + 31) // 32)
+
+
+def set_variant(v):
+    """Select the decode kernel variant (0: 16-leaf register subtree, 1: 8-leaf)."""
+    _lib.check(_lib.lib().pcub_sc_set_variant(int(v)), "pcub_sc_set_variant")
+
+
+class BinaryDecoder:
+    """Batched SC decoder for one CodeSpec; owns its device workspace."""
+
+    def __init__(self, code):
+        self.code = code
+        self._ws = None
+
+    def workspace(self, B):
+        need = int(_lib.lib().pcub_sc_decode_bin_workspace(int(B), self.code.n))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 16), dtype=torch.uint8, device=self.code.device)
+        return self._ws
+
+    def decode_native(self, xy, want_xhat=True, want_u=False, out=None):
+        """xy: [N, B, 2] float64 on device.  Returns packed (info_words, xhat_words|None, u_words|None)."""
+        c = self.code
+        if xy.dtype != torch.float64 or xy.dim() != 3 or xy.shape[0] != c.N or xy.shape[2] != 2:
+            raise ValueError("xy must be float64 [N, B, 2] with N=%d" % c.N)
+        if not xy.is_cuda:
+            raise ValueError("xy must be a device tensor")
+        xy = xy.contiguous()
+        B = xy.shape[1]
+        dev = xy.device
+        if out is None:
+            info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=dev)
+            xh = torch.empty((c.n_words, B), dtype=torch.int32, device=dev) if want_xhat else None
+            uo = torch.empty((c.n_words, B), dtype=torch.int32, device=dev) if want_u else None
+        else:
+            info, xh, uo = out
+        ws = self.workspace(B)
+        rc = _lib.lib().pcub_sc_decode_bin(_p(xy), B, c.n, _p(c.fmask_dev), _p(c.fval_dev), c.K, _p(info), _p(xh),
+                                           _p(uo), _p(ws), ws.numel(), _stream())
+        _lib.check(rc, "pcub_sc_decode_bin")
+        return info, xh, uo
+
+    def decode(self, xy):
+        """xy: [B, N, 2] float64 (per-codeword rows, as the reference's probs).
+        Returns (info [B, K] uint8, xhat [B, N] uint8)."""
+        native = transpose_pairs(xy)
+        info_w, xh_w, _ = self.decode_native(native)
+        return unpack(info_w, self.code.K), unpack(xh_w, self.code.N)
+
+
+def transpose_pairs(xy):
+    """[B, N, q] float64 -> [N, B, q] float64 on device."""
+    if xy.dtype != torch.float64 or xy.dim() != 3:
+        raise ValueError("expected float64 [B, N, q]")
+    xy = xy.contiguous()
+    B, N, q = xy.shape
+    out = torch.empty((N, B, q), dtype=torch.float64, device=xy.device)
+    _lib.check(_lib.lib().pcub_transpose_pairs(_p(xy), B, N, q, _p(out), _stream()), "pcub_transpose_pairs")
+    return out
+
+
+def unpack(words, nbits):
+    """[W, B] int32 words -> [B, nbits] uint8 on device."""
+    W, B = words.shape
+    out = torch.empty((B, nbits), dtype=torch.uint8, device=words.device)
+    _lib.check(_lib.lib().pcub_unpack_bits(_p(words.contiguous()), B, int(nbits), _p(out), _stream()),
+               "pcub_unpack_bits")
+    return out
+
+
+def pack(bits):
+    """[B, nbits] uint8 -> [ceil(nbits/32), B] int32 on device."""
+    bits = bits.to(torch.uint8).contiguous()
+    B, nb = bits.shape
+    out = torch.empty((max(1, (nb + 31) // 32), B), dtype=torch.int32, device=bits.device)
+    _lib.check(_lib.lib().pcub_pack_bits(_p(bits), B, int(nb), _p(out), _stream()), "pcub_pack_bits")
+    return out
+
+
+def encode_native(code, info_words):
+    """Packed info [ceil(K/32), B] -> packed codewords [ceil(N/32), B] (uniform prior)."""
+    B = info_words.shape[1]
+    x = torch.empty((code.n_words, B), dtype=torch.int32, device=info_words.device)
+    rc = _lib.lib().pcub_polar_encode_bin(_p(info_words.contiguous()), B, code.n, _p(code.fmask_dev),
+                                          _p(code.fval_dev), code.K, _p(x), _stream())
+    _lib.check(rc, "pcub_polar_encode_bin")
+    return x
+
+
+def encode(code, info):
+    """info [B, K] uint8 -> codewords [B, N] uint8."""
+    if info.shape[1] != code.K:
+        raise ValueError("info has %d columns, code has K=%d" % (info.shape[1], code.K))
+    if code.K == 0:
+        words = torch.zeros((1, info.shape[0]), dtype=torch.int32, device=info.device)
+    else:
+        words = pack(info)
+    return unpack(encode_native(code, words), code.N)

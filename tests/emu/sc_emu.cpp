@@ -1,0 +1,51 @@
+// Host emulation of the HIP decode schedule (TEST ONLY).
+// Compiles polarcub_amd/csrc/sc_bin_body.h -- the exact code the kernel runs --
+// for the CPU, lane by lane, so schedule/indexing bugs show up in the CPU test
+// suite.  Not part of the product library; nothing in polarcub_amd loads it.
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include "sc_bin_body.h"
+
+using namespace pcub;
+
+extern "C" int emu_decode_bin(const double* xy, long long B, int n, const uint32_t* fmask, const uint32_t* fval,
+                              uint32_t* info, uint32_t* xhat, uint32_t* uout, int S) {
+    const int N = 1 << n;
+    BinArgs A;
+    A.xy = (const double2*)xy;
+    A.B = B;
+    A.n = n;
+    A.fmask = fmask;
+    A.fval = fval;
+    A.info = info;
+    A.xhat = xhat;
+    A.uout = uout;
+    if (n <= 5) {
+        for (long long b = 0; b < B; ++b) {
+            switch (n) {
+                case 0: decode_small<1>(A, b, true); break;
+                case 1: decode_small<2>(A, b, true); break;
+                case 2: decode_small<4>(A, b, true); break;
+                case 3: decode_small<8>(A, b, true); break;
+                case 4: decode_small<16>(A, b, true); break;
+                case 5: decode_small<32>(A, b, true); break;
+            }
+        }
+        return 0;
+    }
+    const long long nslots = 4;  // emulate a few slots, reused across codewords
+    if (N < 2 * S) return -1;
+    std::vector<double2> scr((size_t)(N / 2 - S) * nslots + 1);
+    std::vector<uint32_t> yb((size_t)(N / 32) * nslots);
+    A.scratch = scr.data();
+    A.ybits = yb.data();
+    A.nslots = nslots;
+    for (long long b = 0; b < B; ++b) {
+        if (S == 8) decode_codeword<8>(A, b, b % nslots, true);
+        else if (S == 16) decode_codeword<16>(A, b, b % nslots, true);
+        else decode_codeword<32>(A, b, b % nslots, true);
+    }
+    return 0;
+}

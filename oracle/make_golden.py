@@ -378,6 +378,46 @@ def fx_qsc(R, timing):
     save("qary_q3_n32", dict(q=q3, N=N3), frozen=m3, xy=x3, info=info3, enc_info=tx3.astype(np.uint8), enc_x=enc3)
 
 
+def fx_harness(R, timing):
+    """The reference's own Monte-Carlo driver (encodeDecodeSimulation, BinaryPolarEncoderDecoder.py:328-387)
+    with test2.py-style BSC closures and an explicitly seeded global RNG; records the printed line."""
+    import contextlib
+    import io
+    BMD, BPED = R["BMD"], R["BPED"]
+    g = np.load(os.path.join(OUT, "bsc_n64.npz"))
+    frozen = set(int(i) for i in np.nonzero(g["frozen"])[0])
+    N, T, seed = 64, 400, 5
+    xy_dist = BMD.makeBSC(0.11)
+
+    def make_x():
+        xd = BMD.BinaryMemorylessDistribution()
+        xd.probs.append([xy_dist.calcXMarginal(0), xy_dist.calcXMarginal(1)])
+        return xd.makeBinaryMemorylessVectorDistribution(N, None)
+
+    def channel(codeword):  # test2.py:29-50
+        out = []
+        for x in codeword:
+            rnd = random.random()
+            s = 0.0
+            for y in range(len(xy_dist.probs)):
+                if s + xy_dist.probXGivenY(x, y) >= rnd:
+                    out.append(y)
+                    break
+                s += xy_dist.probXGivenY(x, y)
+        return out
+
+    def make_xy(received):
+        return xy_dist.makeBinaryMemorylessVectorDistribution(len(received), received)
+
+    random.seed(seed)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        BPED.encodeDecodeSimulation(N, make_x, lambda e: e, channel, make_xy, T, frozen)
+    line = buf.getvalue().strip().splitlines()[-1]
+    print("  reference printed:", line)
+    save("harness_bsc_n64", dict(N=N, trials=T, global_seed=seed, p=0.11, line=line), frozen=g["frozen"])
+
+
 FIXTURES = {
     "bsc_n64": fx_bsc_n64,
     "awgn_n1024": lambda R, t: fx_awgn(R, t, 10, 64, 2.0, 20250204, "awgn_n1024", "C2"),
@@ -387,6 +427,7 @@ FIXTURES = {
     "prior_n64": fx_prior,
     "encode_binary": fx_encode,
     "qsc_q4_n256": fx_qsc,
+    "harness_bsc_n64": fx_harness,
 }
 
 

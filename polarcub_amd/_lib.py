@@ -34,6 +34,10 @@ def lib():
     L.pcub_abi_version.argtypes = []
     L.pcub_sc_set_variant.restype = ctypes.c_int
     L.pcub_sc_set_variant.argtypes = [ctypes.c_int]
+    L.pcub_sc_num_variants.restype = ctypes.c_int
+    L.pcub_sc_num_variants.argtypes = []
+    L.pcub_sc_variant_info.restype = ctypes.c_int
+    L.pcub_sc_variant_info.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_int)] * 3
     L.pcub_sc_decode_bin_workspace.restype = ctypes.c_size_t
     L.pcub_sc_decode_bin_workspace.argtypes = [_i64, _i32]
     L.pcub_sc_decode_bin.restype = ctypes.c_int

@@ -22,20 +22,27 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// Variants: register-subtree length S and the minimum waves/SIMD the register
-// allocation must allow (launch-bounds).  Variant 0 is the default.
-//   0: S = 16, 2 waves/SIMD (219 VGPRs)     1: S = 8, 4 waves/SIMD (124 VGPRs)
-constexpr int kNumVariants = 2;
-constexpr int kVarS[kNumVariants] = {16, 8};
+// Decode kernel variants: virtual register subtree S (values per lane), lanes
+// per codeword G, and the minimum waves/SIMD the register allocation must allow.
+struct Variant {
+    int S, G, W;
+};
+constexpr int kNumVariants = 7;
+constexpr Variant kVar[kNumVariants] = {
+    {16, 1, 2}, {8, 1, 4}, {16, 2, 2}, {16, 4, 2}, {8, 4, 4}, {8, 8, 4}, {8, 2, 4},
+};
 
-template <int S, int W>
+template <int S, int G, int W>
 __global__ __launch_bounds__(kBlock, W) void k_sc_bin(BinArgs A) {
+    constexpr int CWB = kBlock / G;  // codewords per workgroup tile
     const long long slot = (long long)blockIdx.x * kBlock + threadIdx.x;
-    const long long ntiles = (A.B + kBlock - 1) / kBlock;
+    const int j = threadIdx.x & (G - 1);
+    const int lane = threadIdx.x & 63;
+    const long long ntiles = (A.B + CWB - 1) / CWB;
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const long long cw = t * kBlock + threadIdx.x;
+        const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_codeword<S>(A, valid ? cw : A.B - 1, slot, valid);
+        decode_codeword<S, G>(A, valid ? cw : A.B - 1, j, lane, slot, valid);
     }
 }
 
@@ -47,7 +54,15 @@ __global__ __launch_bounds__(kBlock) void k_sc_bin_small(BinArgs A) {
 
 typedef void (*KernFn)(BinArgs);
 KernFn variant_kernel(int v) {
-    return v == 1 ? k_sc_bin<8, 4> : k_sc_bin<16, 2>;
+    switch (v) {
+        case 1: return k_sc_bin<8, 1, 4>;
+        case 2: return k_sc_bin<16, 2, 2>;
+        case 3: return k_sc_bin<16, 4, 2>;
+        case 4: return k_sc_bin<8, 4, 4>;
+        case 5: return k_sc_bin<8, 8, 4>;
+        case 6: return k_sc_bin<8, 2, 4>;
+        default: return k_sc_bin<16, 1, 2>;
+    }
 }
 
 int g_variant = 0;
@@ -55,7 +70,7 @@ int g_variant = 0;
 struct DevInfo {
     int dev = -1;
     int cus = 0;
-    int occ[kNumVariants] = {0, 0};
+    int occ[kNumVariants] = {};
 };
 
 DevInfo dev_info() {
@@ -76,23 +91,27 @@ DevInfo dev_info() {
     return d;
 }
 
-size_t slot_bytes(int n, int S) {
-    const size_t N = (size_t)1 << n;
-    return (N / 2 - S) * sizeof(double2) + (N / 32) * sizeof(uint32_t);
+// per-slot bytes: virtual levels 1..D-1 (Nv/2 - S pairs) + Nv local encoding bits
+size_t slot_bytes(int n, int v) {
+    const size_t Nv = ((size_t)1 << n) / kVar[v].G;
+    return (Nv / 2 - kVar[v].S) * sizeof(double2) + (Nv / 32) * sizeof(uint32_t);
 }
 
 long long grid_for(long long B, int v) {
     const DevInfo d = dev_info();
     if (d.cus <= 0) return 0;
-    const long long ntiles = (B + kBlock - 1) / kBlock;
+    const long long cwb = kBlock / kVar[v].G;
+    const long long ntiles = (B + cwb - 1) / cwb;
     long long g = (long long)d.cus * d.occ[v];
     return ntiles < g ? ntiles : g;
 }
 
-// the subtree must leave at least one outer level: N >= 2S
+// a variant needs at least one outer level (N >= 2*S*G) and whole-word x_hat
+// segments (N >= 32*G); otherwise fall back to the 8-leaf one-lane variant.
 int pick_variant(int n) {
     int v = g_variant;
-    if ((1 << n) < 2 * kVarS[v]) v = 1;
+    const long long N = 1LL << n;
+    if (N < 2LL * kVar[v].S * kVar[v].G || N < 32LL * kVar[v].G) v = 1;
     return v;
 }
 
@@ -100,7 +119,15 @@ int pick_variant(int n) {
 
 extern "C" int pcub_abi_version(void) { return 1; }
 
-// Tuning hook (not part of the stable ABI): choose the decode kernel variant.
+// Tuning hooks (not part of the stable ABI): choose / describe the decode kernel variant.
+extern "C" int pcub_sc_num_variants(void) { return kNumVariants; }
+extern "C" int pcub_sc_variant_info(int v, int* S, int* G, int* W) {
+    if (v < 0 || v >= kNumVariants) return PCUB_EINVAL;
+    *S = kVar[v].S;
+    *G = kVar[v].G;
+    *W = kVar[v].W;
+    return 0;
+}
 extern "C" int pcub_sc_set_variant(int v) {
     if (v < 0 || v >= kNumVariants) return PCUB_EINVAL;
     g_variant = v;
@@ -112,7 +139,7 @@ extern "C" size_t pcub_sc_decode_bin_workspace(int64_t B, int32_t log2N) {
     if (log2N < 6) return 0;
     const int v = pick_variant(log2N);
     const long long g = grid_for(B, v);
-    return (size_t)g * kBlock * slot_bytes(log2N, kVarS[v]);
+    return (size_t)g * kBlock * slot_bytes(log2N, v);
 }
 
 extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
@@ -147,18 +174,17 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
         return (int)hipGetLastError();
     }
     const int v = pick_variant(log2N);
-    const int S = kVarS[v];
     long long g = grid_for(B, v);
     if (g <= 0) return (int)hipErrorNoDevice;
-    const size_t per_block = (size_t)kBlock * slot_bytes(log2N, S);
+    const size_t per_block = (size_t)kBlock * slot_bytes(log2N, v);
     if (!workspace) return PCUB_EINVAL;
     if ((size_t)g * per_block > workspace_bytes) g = (long long)(workspace_bytes / per_block);
     if (g <= 0) return PCUB_EINVAL;
     const long long nslots = g * kBlock;
-    const size_t N = (size_t)1 << log2N;
+    const size_t Nv = ((size_t)1 << log2N) / kVar[v].G;
     A.nslots = nslots;
     A.scratch = (double2*)workspace;
-    A.ybits = (uint32_t*)((char*)workspace + (size_t)nslots * (N / 2 - S) * sizeof(double2));
+    A.ybits = (uint32_t*)((char*)workspace + (size_t)nslots * (Nv / 2 - kVar[v].S) * sizeof(double2));
     hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), 0, st, A);
     return (int)hipGetLastError();
 }

@@ -108,8 +108,20 @@ class CodeSpec:
 
 
 def set_variant(v):
-    """Select the decode kernel variant (0: 16-leaf register subtree, 1: 8-leaf)."""
+    """Select the decode kernel variant (see variants())."""
     _lib.check(_lib.lib().pcub_sc_set_variant(int(v)), "pcub_sc_set_variant")
+
+
+def variants():
+    """[(S, G, W)] per decode kernel variant: register-subtree values per lane,
+    lanes per codeword, minimum waves per SIMD."""
+    L = _lib.lib()
+    out = []
+    for v in range(L.pcub_sc_num_variants()):
+        S, G, W = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(L.pcub_sc_variant_info(v, ctypes.byref(S), ctypes.byref(G), ctypes.byref(W)), "variant_info")
+        out.append((S.value, G.value, W.value))
+    return out
 
 
 class BinaryDecoder:

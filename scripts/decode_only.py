@@ -1,0 +1,32 @@
+"""Minimal driver for profiling: generate the bench workload, run the decode kernel R times."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from polarcub_amd import construction, sc  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=10)
+ap.add_argument("--batch", type=int, default=1 << 20)
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--variant", type=int, default=0)
+a = ap.parse_args()
+N = 1 << a.n
+K = N // 2
+s2 = construction.awgn_sigma2(2.0, 0.5)
+fr = construction.bhattacharyya_frozen(a.n, K, s2)
+code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(fr)[0].tolist()), 1)
+sc.set_variant(a.variant)
+dec = sc.BinaryDecoder(code)
+xy, info = bench.make_inputs(code, a.batch, s2, 1, torch.device("cuda"))
+outs = (torch.empty((code.info_words, a.batch), dtype=torch.int32, device="cuda"),
+        torch.empty((code.n_words, a.batch), dtype=torch.int32, device="cuda"), None)
+for _ in range(a.reps):
+    dec.decode_native(xy, out=outs)
+torch.cuda.synchronize()
+print("done")

@@ -43,9 +43,9 @@ extern "C" int emu_decode_bin(const double* xy, long long B, int n, const uint32
     A.ybits = yb.data();
     A.nslots = nslots;
     for (long long b = 0; b < B; ++b) {
-        if (S == 8) decode_codeword<8>(A, b, b % nslots, true);
-        else if (S == 16) decode_codeword<16>(A, b, b % nslots, true);
-        else decode_codeword<32>(A, b, b % nslots, true);
+        if (S == 8) decode_codeword<8, 1>(A, b, 0, 0, b % nslots, true);
+        else if (S == 16) decode_codeword<16, 1>(A, b, 0, 0, b % nslots, true);
+        else decode_codeword<32, 1>(A, b, 0, 0, b % nslots, true);
     }
     return 0;
 }

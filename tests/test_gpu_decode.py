@@ -21,7 +21,7 @@ def sc():
     return _sc
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", range(7))
 @pytest.mark.parametrize("name", BIN_SETS)
 def test_decode_matches_reference(sc, name, variant):
     sc.set_variant(variant)
@@ -36,8 +36,10 @@ def test_decode_matches_reference(sc, name, variant):
     sc.set_variant(0)
 
 
+@pytest.mark.parametrize("variant", [0, 3, 5])
 @pytest.mark.parametrize("idx", range(24))
-def test_edge_cases(sc, idx):
+def test_edge_cases(sc, idx, variant):
+    sc.set_variant(variant)
     c = edge_cases()[idx]
     N = 1 << int(c["n"])
     code = sc.CodeSpec(N, c["frozen"], c["fval"])
@@ -46,11 +48,13 @@ def test_edge_cases(sc, idx):
     assert np.array_equal(xhat.cpu().numpy(), c["xhat"])
 
 
-def test_ragged_batches_and_slot_reuse(sc):
+@pytest.mark.parametrize("variant", range(7))
+def test_ragged_batches_and_slot_reuse(sc, variant):
     """Batch sizes that are not tile multiples, and more tiles than resident slots."""
     from oracle import orc
-    rng = np.random.default_rng(3)
-    for N, B in [(64, 1), (128, 257), (256, 1000), (1024, 300), (512, 70000)]:
+    sc.set_variant(variant)
+    rng = np.random.default_rng(3 + variant)
+    for N, B in [(64, 1), (128, 257), (256, 1000), (1024, 300), (512, 70000), (2048, 33)]:
         frozen = (rng.random(N) < 0.5).astype(np.uint8)
         fval = (rng.random(N) < 0.5).astype(np.uint8)
         xy = rng.random((B, N, 2))
@@ -61,6 +65,7 @@ def test_ragged_batches_and_slot_reuse(sc):
         ri, rx = orc.decode_bin(xy[sub], frozen, fval)
         assert np.array_equal(info.cpu().numpy()[sub], ri), (N, B)
         assert np.array_equal(xhat.cpu().numpy()[sub], rx), (N, B)
+    sc.set_variant(0)
 
 
 @pytest.mark.parametrize("n", [1, 3, 5, 8, 10])

@@ -1,0 +1,83 @@
+"""The reference-compatible facade on the GPU: decode()/encode() and the
+Monte-Carlo driver must reproduce the reference's outputs and printed line."""
+import contextlib
+import io
+import random
+
+import numpy as np
+import pytest
+
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def test_facade_decode_matches_reference():
+    from polarcub_amd import coding, scalar, vectors
+    for name in ("bsc_n64", "awgn_n1024"):
+        g = load_golden(name)
+        N = g["frozen"].shape[0]
+        xy = g["xy"] if "xy" in g else g["table"][g["y"]]
+        fs = set(int(i) for i in np.nonzero(g["frozen"])[0])
+        enc = coding.BinaryPolarEncoderDecoder(N, fs, g["meta"]["crs"])
+        xvd = vectors.BinaryMemorylessVectorDistribution(N)
+        xvd.probs[:] = 0.5
+        for b in range(0, xy.shape[0], max(1, xy.shape[0] // 16)):
+            yvd = vectors.BinaryMemorylessVectorDistribution(N)
+            yvd.probs[:] = xy[b]
+            x, info = enc.decode(xvd, yvd)
+            assert x.dtype == np.int64 and info.dtype == np.int64
+            assert np.array_equal(info, g["info"][b])
+            assert np.array_equal(x, g["xhat"][b])
+        X, I = enc.decode_batch(xy)
+        assert np.array_equal(I, g["info"]) and np.array_equal(X, g["xhat"])
+
+
+def test_facade_encode_matches_reference():
+    from polarcub_amd import coding, vectors
+    g = load_golden("encode_binary")
+    for n in (3, 8, 10):
+        N = 1 << n
+        fs = set(int(i) for i in np.nonzero(g["n%d_frozen" % n])[0])
+        # frozen values come from r_i; rebuild them through the seed-free path by checking equality
+        enc = coding.BinaryPolarEncoderDecoder(N, fs, 0)
+        enc.randomlyGeneratedNumbers = g["n%d_r" % n]
+        xvd = vectors.BinaryMemorylessVectorDistribution(N)
+        xvd.probs[:] = 0.5
+        for b in range(g["n%d_info" % n].shape[0]):
+            assert np.array_equal(enc.encode(xvd, list(g["n%d_info" % n][b])), g["n%d_x" % n][b])
+
+
+def test_encode_decode_simulation_prints_reference_line():
+    from polarcub_amd import coding, scalar
+    g = load_golden("harness_bsc_n64")
+    m = g["meta"]
+    N = m["N"]
+    fs = set(int(i) for i in np.nonzero(g["frozen"])[0])
+    xy_dist = scalar.makeBSC(m["p"])
+
+    def make_x():
+        xd = scalar.BinaryMemorylessDistribution()
+        xd.probs.append([xy_dist.calcXMarginal(0), xy_dist.calcXMarginal(1)])
+        return xd.makeBinaryMemorylessVectorDistribution(N, None)
+
+    def channel(codeword):
+        out = []
+        for x in codeword:
+            rnd = random.random()
+            s = 0.0
+            for y in range(len(xy_dist.probs)):
+                if s + xy_dist.probXGivenY(x, y) >= rnd:
+                    out.append(y)
+                    break
+                s += xy_dist.probXGivenY(x, y)
+        return out
+
+    def make_xy(received):
+        return xy_dist.makeBinaryMemorylessVectorDistribution(len(received), received)
+
+    random.seed(m["global_seed"])
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        coding.encodeDecodeSimulation(N, make_x, lambda e: e, channel, make_xy, m["trials"], fs)
+    assert buf.getvalue().strip().splitlines()[-1] == m["line"]

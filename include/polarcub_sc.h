@@ -67,6 +67,21 @@ int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, const uint32_
                        const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
                        uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream);
 
+/* q-ary SC decode (linear domain), 2 <= q <= 8, N >= 4.
+ *   xy        [N][B][q] f64 joint probabilities P(X_i = x, Y_i = y_i)
+ *   frozen    [N] u8 (1 = frozen; frozen symbols are 0, QaryPolarEncoderDecoder.py:351)
+ *   info      out [K][B] u8 decoded information symbols in u order
+ *   xhat      out [N][B] u8 re-encoded codeword estimate (may be NULL)
+ *   workspace pcub_sc_decode_qary_workspace(B, log2N, q) bytes */
+size_t pcub_sc_decode_qary_workspace(int64_t B, int32_t log2N, int32_t q);
+int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, int32_t q, const uint8_t* frozen, int32_t K,
+                        uint8_t* info, uint8_t* xhat, void* workspace, size_t workspace_bytes, void* stream);
+
+/* q-ary polar encoder (QaryPolarEncoderDecoder.py:65-88, frozen symbols 0):
+ *   info [K][B] u8 -> x [N][B] u8, combine x[2h] = (xm+xp)%q, x[2h+1] = (q-xp)%q. */
+int pcub_polar_encode_qary(const uint8_t* info, int64_t B, int32_t log2N, int32_t q, const uint8_t* frozen, int32_t K,
+                           uint8_t* x, void* stream);
+
 /* Polar encoder (uniform prior): u_i = frozen_val_i at frozen positions, the
  * next information bit elsewhere; x = polar transform of u in the reference's
  * adjacent-pair convention (BinaryPolarEncoderDecoder.py:319-323, :494-516).
@@ -78,7 +93,7 @@ int pcub_polar_encode_bin(const uint32_t* info_words, int64_t B, int32_t log2N, 
 int pcub_pack_bits(const uint8_t* bits, int64_t B, int32_t nbits, uint32_t* words, void* stream);
 int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits, uint8_t* bits, void* stream);
 
-/* [B][N][q] f64 -> [N][B][q] f64 (q = 2 for binary pairs). */
+/* [B][N][q] f64 -> [N][B][q] f64, 1 <= q <= 8 (q = 2 for binary pairs). */
 int pcub_transpose_pairs(const double* src, int64_t B, int32_t N, int32_t q, double* dst, void* stream);
 
 #ifdef __cplusplus

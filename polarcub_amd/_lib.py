@@ -43,6 +43,13 @@ def lib():
     L.pcub_sc_decode_bin.restype = ctypes.c_int
     L.pcub_sc_decode_bin.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                                      _c_void_p, _c_void_p, ctypes.c_size_t, _c_void_p]
+    L.pcub_sc_decode_qary_workspace.restype = ctypes.c_size_t
+    L.pcub_sc_decode_qary_workspace.argtypes = [_i64, _i32, _i32]
+    L.pcub_sc_decode_qary.restype = ctypes.c_int
+    L.pcub_sc_decode_qary.argtypes = [_c_void_p, _i64, _i32, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                      ctypes.c_size_t, _c_void_p]
+    L.pcub_polar_encode_qary.restype = ctypes.c_int
+    L.pcub_polar_encode_qary.argtypes = [_c_void_p, _i64, _i32, _i32, _c_void_p, _i32, _c_void_p, _c_void_p]
     L.pcub_polar_encode_bin.restype = ctypes.c_int
     L.pcub_polar_encode_bin.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p]
     L.pcub_pack_bits.restype = ctypes.c_int
@@ -59,6 +66,7 @@ def lib():
 
 # every exported symbol declared in include/polarcub_sc.h
 EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_bin", "pcub_polar_encode_bin",
+           "pcub_sc_decode_qary_workspace", "pcub_sc_decode_qary", "pcub_polar_encode_qary",
            "pcub_pack_bits", "pcub_unpack_bits", "pcub_transpose_pairs"]
 
 

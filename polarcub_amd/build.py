@@ -17,7 +17,7 @@ LIB = os.path.join(PKG, "lib", "libpolarcub_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PCUB_ARCH", "gfx950")
 
-SOURCES = ["sc_bin.hip", "sc_util.hip"]
+SOURCES = ["sc_bin.hip", "sc_qary.hip", "sc_util.hip"]
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
          "-std=c++17", "-Wall", "-Wno-unused-function"]
 

@@ -93,24 +93,28 @@ __global__ void k_unpack_bits(const uint32_t* __restrict__ words, long long B, i
     bits[idx] = (uint8_t)((words[(long long)(i >> 5) * B + b] >> (i & 31)) & 1u);
 }
 
-// [B][N][q] -> [N][B][q] through a 32x32-element LDS tile.
-__global__ void k_transpose(const double* __restrict__ src, long long B, int N, int q, double* __restrict__ dst) {
-    __shared__ double tile[32][33 * 4];
+// [B][N][q] -> [N][B][q] through a 32 (codewords) x 16 (positions) LDS tile, q <= 8.
+__global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ src, long long B, int N, int q,
+                                                  double* __restrict__ dst) {
+    __shared__ double tile[32][16 * 8 + 1];
     const long long b0 = (long long)blockIdx.x * 32;
-    const int i0 = blockIdx.y * 32;
-    const int tx = threadIdx.x, ty = threadIdx.y;  // 32 x 8
-    for (int r = ty; r < 32; r += 8) {
+    const int i0 = blockIdx.y * 16;
+    const int t = threadIdx.x;
+    // load: rows b (32), each row a contiguous run of 16*q doubles
+    for (int e = t; e < 32 * 16 * q; e += 256) {
+        const int r = e / (16 * q), c = e % (16 * q);
         const long long b = b0 + r;
-        const int i = i0 + tx;
-        if (b < B && i < N)
-            for (int c = 0; c < q; ++c) tile[r][tx * q + c] = src[(b * N + i) * q + c];
+        const int i = i0 + c / q;
+        if (b < B && i < N) tile[r][c] = src[(b * N + i0) * q + c];
     }
     __syncthreads();
-    for (int r = ty; r < 32; r += 8) {
-        const int i = i0 + r;
-        const long long b = b0 + tx;
-        if (b < B && i < N)
-            for (int c = 0; c < q; ++c) dst[((long long)i * B + b) * q + c] = tile[tx][r * q + c];
+    // store: for each position i, a contiguous run of 32*q doubles (codewords b0..b0+31)
+    for (int e = t; e < 16 * 32 * q; e += 256) {
+        const int ii = e / (32 * q), c = e % (32 * q);
+        const int r = c / q, x = c % q;
+        const long long b = b0 + r;
+        const int i = i0 + ii;
+        if (b < B && i < N) dst[((long long)i * B + b0) * q + c] = tile[r][ii * q + x];
     }
 }
 
@@ -147,9 +151,9 @@ extern "C" int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits,
 }
 
 extern "C" int pcub_transpose_pairs(const double* src, int64_t B, int32_t N, int32_t q, double* dst, void* stream) {
-    if (B < 0 || N < 0 || q < 1 || q > 4 || (B > 0 && N > 0 && (!src || !dst))) return PCUB_EINVAL;
+    if (B < 0 || N < 0 || q < 1 || q > 8 || (B > 0 && N > 0 && (!src || !dst))) return PCUB_EINVAL;
     if (B == 0 || N == 0) return 0;
-    const dim3 grid((unsigned)((B + 31) / 32), (unsigned)((N + 31) / 32));
-    hipLaunchKernelGGL(k_transpose, grid, dim3(32, 8), 0, (hipStream_t)stream, src, (long long)B, N, q, dst);
+    const dim3 grid((unsigned)((B + 31) / 32), (unsigned)((N + 15) / 16));
+    hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, (hipStream_t)stream, src, (long long)B, N, q, dst);
     return (int)hipGetLastError();
 }

@@ -215,3 +215,72 @@ def encode(code, info):
     else:
         words = pack(info)
     return unpack(encode_native(code, words), code.N)
+
+
+class QaryCode:
+    """One q-ary polar code (2 <= q <= 8): length, frozen positions (frozen symbols are 0,
+    QaryPolarEncoderDecoder.py:347-351), resident on the device."""
+
+    def __init__(self, q, N, frozen_mask, device=None):
+        self.q = int(q)
+        if not 2 <= self.q <= 8:
+            raise ValueError("q must be in [2, 8] for the device decoder")
+        self.N = int(N)
+        self.n = _log2(self.N)
+        if self.n < 2:
+            raise ValueError("q-ary device decoder needs N >= 4")
+        mask = (np.asarray(frozen_mask, dtype=np.uint8).reshape(-1) != 0).astype(np.uint8)
+        if mask.shape[0] != self.N:
+            raise ValueError("frozen mask has %d entries, expected N=%d" % (mask.shape[0], self.N))
+        self.frozen_mask = mask
+        self.K = int(self.N - int(mask.sum()))
+        self.device = torch.device("cuda") if device is None else torch.device(device)
+        self.frozen_dev = torch.from_numpy(mask.copy()).to(self.device)
+
+
+class QaryDecoder:
+    """Batched q-ary SC decoder for one QaryCode (linear-domain probabilities)."""
+
+    def __init__(self, code):
+        self.code = code
+        self._ws = None
+
+    def workspace(self, B):
+        c = self.code
+        need = int(_lib.lib().pcub_sc_decode_qary_workspace(int(B), c.n, c.q))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 16), dtype=torch.uint8, device=c.device)
+        return self._ws
+
+    def decode_native(self, xy, want_xhat=True):
+        """xy: [N, B, q] float64 on device -> (info [K, B] uint8, xhat [N, B] uint8 | None)."""
+        c = self.code
+        if xy.dtype != torch.float64 or xy.dim() != 3 or xy.shape[0] != c.N or xy.shape[2] != c.q:
+            raise ValueError("xy must be float64 [N, B, q] with N=%d, q=%d" % (c.N, c.q))
+        xy = xy.contiguous()
+        B = xy.shape[1]
+        info = torch.empty((max(1, c.K), B), dtype=torch.uint8, device=xy.device)
+        xh = torch.empty((c.N, B), dtype=torch.uint8, device=xy.device) if want_xhat else None
+        ws = self.workspace(B)
+        rc = _lib.lib().pcub_sc_decode_qary(_p(xy), B, c.n, c.q, _p(c.frozen_dev), c.K, _p(info), _p(xh), _p(ws),
+                                            ws.numel(), _stream())
+        _lib.check(rc, "pcub_sc_decode_qary")
+        return info[:c.K], xh
+
+    def decode(self, xy):
+        """xy: [B, N, q] float64 -> (info [B, K] uint8, xhat [B, N] uint8)."""
+        info, xh = self.decode_native(transpose_pairs(xy))
+        return info.t().contiguous(), xh.t().contiguous()
+
+
+def encode_qary(code, info):
+    """info [B, K] uint8 symbols -> codewords [B, N] uint8."""
+    B = info.shape[0]
+    if info.shape[1] != code.K:
+        raise ValueError("info has %d columns, code has K=%d" % (info.shape[1], code.K))
+    inf = info.to(torch.uint8).t().contiguous() if code.K else torch.zeros((1, B), dtype=torch.uint8,
+                                                                          device=code.device)
+    x = torch.empty((code.N, B), dtype=torch.uint8, device=code.device)
+    rc = _lib.lib().pcub_polar_encode_qary(_p(inf), B, code.n, code.q, _p(code.frozen_dev), code.K, _p(x), _stream())
+    _lib.check(rc, "pcub_polar_encode_qary")
+    return x.t().contiguous()

@@ -109,3 +109,30 @@ def test_dropin_tree_imports():
         assert V.BinaryMemorylessVectorDistribution is vectors.BinaryMemorylessVectorDistribution
     finally:
         sys.path.remove(d)
+
+
+def test_qary_polar_transform_and_generic_recursion():
+    from polarcub_amd import coding_qary, scalar_qary
+    g = load_golden("qsc_q4_n256")
+    fz = g["frozen"]
+    for t in range(0, 160, 40):
+        u = coding_qary.polarTransformOfQudits(4, g["x"][t])
+        assert np.array_equal(u[fz == 0], g["tx_info"][t]) and np.all(u[fz == 1] == 0)
+    fs = set(int(i) for i in np.nonzero(fz)[0])
+    encdec = coding_qary.QaryPolarEncoderDecoder(4, 256, fs, 1)
+    qsc = scalar_qary.makeQSC(4, 0.11)
+    xvd = vectors.QaryMemorylessVectorDistribution(4, 256)
+    xvd.probs[:] = 0.25
+    for t in range(0, 160, 53):
+        yvd = qsc.makeQaryMemorylessVectorDistribution(256, [int(v) for v in g["y"][t]])
+        info = np.full(encdec.k, -1, np.int64)
+        encdec.recursiveEncodeDecode(info, 0, 0, xvd, yvd)
+        assert np.array_equal(info, g["info"][t])
+
+
+def test_qary_frozen_set_quirks():
+    from polarcub_amd import coding_qary
+    pe = [0.5, 0.1, 0.3, 0.0, 0.2, 0.05, 0.4, 0.01]
+    fs = coding_qary.frozenSetFromTVAndPe([0.0] * 8, pe, numInfoIndices=2)
+    # numInfoIndices=2 keeps 3 information indices (the reference's off-by-one)
+    assert fs == {0, 2, 4, 6, 1}

@@ -1,0 +1,72 @@
+"""q-ary SC on the GPU against the reference's golden vectors (bit-exact symbols)."""
+import numpy as np
+import pytest
+
+from tests.conftest import load_golden
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def test_qsc_q4_n256_matches_reference():
+    from polarcub_amd import sc
+    g = load_golden("qsc_q4_n256")
+    code = sc.QaryCode(4, 256, g["frozen"])
+    dec = sc.QaryDecoder(code)
+    info, xhat = dec.decode(torch.from_numpy(g["table"][g["y"]]).cuda())
+    assert np.array_equal(info.cpu().numpy(), g["info"])
+    info_r, _ = dec.decode(torch.from_numpy(g["xy_rand"]).cuda())
+    assert np.array_equal(info_r.cpu().numpy(), g["info_rand"])
+    # x_hat re-encodes the decoded symbols
+    enc = sc.encode_qary(code, info)
+    assert torch.equal(enc, xhat)
+
+
+def test_qary_q3_matches_reference():
+    from polarcub_amd import sc
+    g = load_golden("qary_q3_n32")
+    code = sc.QaryCode(3, 32, g["frozen"])
+    info, _ = sc.QaryDecoder(code).decode(torch.from_numpy(g["xy"]).cuda())
+    assert np.array_equal(info.cpu().numpy(), g["info"])
+    x = sc.encode_qary(code, torch.from_numpy(g["enc_info"]).cuda())
+    assert np.array_equal(x.cpu().numpy(), g["enc_x"])
+
+
+def test_qary_encode_matches_reference():
+    from polarcub_amd import sc
+    g = load_golden("qsc_q4_n256")
+    code = sc.QaryCode(4, 256, g["frozen"])
+    x = sc.encode_qary(code, torch.from_numpy(g["tx_info"]).cuda())
+    assert np.array_equal(x.cpu().numpy(), g["x"])
+
+
+@pytest.mark.parametrize("q", [2, 3, 4, 5, 8])
+def test_qary_random_vs_oracle(q):
+    from oracle import orc
+    from polarcub_amd import sc
+    rng = np.random.default_rng(q)
+    for N, B in [(4, 7), (64, 300), (512, 1000)]:
+        frozen = (rng.random(N) < 0.4).astype(np.uint8)
+        xy = rng.random((B, N, q))
+        xy[rng.random((B, N)) < 0.05] = 0.0
+        code = sc.QaryCode(q, N, frozen)
+        info, xhat = sc.QaryDecoder(code).decode(torch.from_numpy(xy).cuda())
+        ri, rx = orc.decode_qary(q, xy, frozen)
+        assert np.array_equal(info.cpu().numpy(), ri), (q, N)
+        assert np.array_equal(xhat.cpu().numpy(), rx), (q, N)
+
+
+def test_qary_facade_decode():
+    from polarcub_amd import coding_qary, scalar_qary
+    g = load_golden("qsc_q4_n256")
+    fs = set(int(i) for i in np.nonzero(g["frozen"])[0])
+    encdec = coding_qary.QaryPolarEncoderDecoder(4, 256, fs, 1)
+    qsc = scalar_qary.makeQSC(4, 0.11)
+    xq = scalar_qary.QaryMemorylessDistribution(4)
+    xq.probs = [qsc.calcXMarginals()]
+    xvd = xq.makeQaryMemorylessVectorDistribution(256, None)
+    for t in range(0, 160, 20):
+        yvd = qsc.makeQaryMemorylessVectorDistribution(256, [int(v) for v in g["y"][t]])
+        info = encdec.decode(xvd, yvd)
+        assert info.dtype == np.int64 and np.array_equal(info, g["info"][t])
+    assert np.array_equal(encdec.encode(xvd, list(g["tx_info"][0])), g["x"][0])

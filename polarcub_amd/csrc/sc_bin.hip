@@ -24,25 +24,31 @@ constexpr int kBlock = 256;
 
 // Decode kernel variants: virtual register subtree S (values per lane), lanes
 // per codeword G, and the minimum waves/SIMD the register allocation must allow.
+// LDS: the deepest stage level (depth D-1, 2S values per lane) lives in LDS.
 struct Variant {
-    int S, G, W;
+    int S, G, W, L;
 };
-constexpr int kNumVariants = 7;
+constexpr int kNumVariants = 13;
 constexpr Variant kVar[kNumVariants] = {
-    {16, 1, 2}, {8, 1, 4}, {16, 2, 2}, {16, 4, 2}, {8, 4, 4}, {8, 8, 4}, {8, 2, 4},
+    {16, 1, 2, 0}, {8, 1, 4, 0}, {32, 1, 1, 0}, {16, 4, 2, 0}, {8, 4, 4, 0}, {16, 2, 2, 0}, {32, 2, 1, 0},
+    {8, 4, 4, 1},  {16, 1, 2, 1}, {16, 4, 2, 1}, {32, 1, 1, 1}, {32, 2, 1, 1}, {16, 2, 2, 1},
 };
 
-template <int S, int G, int W>
+size_t lds_bytes(int v) { return kVar[v].L ? (size_t)kVar[v].S * kBlock * sizeof(double2) : 0; }
+
+template <int S, int G, int W, bool LDS>
 __global__ __launch_bounds__(kBlock, W) void k_sc_bin(BinArgs A) {
+    extern __shared__ double2 lds_last[];  // [S pairs][kBlock] when LDS
     constexpr int CWB = kBlock / G;  // codewords per workgroup tile
     const long long slot = (long long)blockIdx.x * kBlock + threadIdx.x;
     const int j = threadIdx.x & (G - 1);
     const int lane = threadIdx.x & 63;
+    const Lvl last = LDS ? Lvl{lds_last + threadIdx.x, kBlock} : Lvl{nullptr, 0};
     const long long ntiles = (A.B + CWB - 1) / CWB;
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_codeword<S, G>(A, valid ? cw : A.B - 1, j, lane, slot, valid);
+        decode_codeword<S, G, LDS>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last);
     }
 }
 
@@ -55,13 +61,19 @@ __global__ __launch_bounds__(kBlock) void k_sc_bin_small(BinArgs A) {
 typedef void (*KernFn)(BinArgs);
 KernFn variant_kernel(int v) {
     switch (v) {
-        case 1: return k_sc_bin<8, 1, 4>;
-        case 2: return k_sc_bin<16, 2, 2>;
-        case 3: return k_sc_bin<16, 4, 2>;
-        case 4: return k_sc_bin<8, 4, 4>;
-        case 5: return k_sc_bin<8, 8, 4>;
-        case 6: return k_sc_bin<8, 2, 4>;
-        default: return k_sc_bin<16, 1, 2>;
+        case 1: return k_sc_bin<8, 1, 4, false>;
+        case 2: return k_sc_bin<32, 1, 1, false>;
+        case 3: return k_sc_bin<16, 4, 2, false>;
+        case 4: return k_sc_bin<8, 4, 4, false>;
+        case 5: return k_sc_bin<16, 2, 2, false>;
+        case 6: return k_sc_bin<32, 2, 1, false>;
+        case 7: return k_sc_bin<8, 4, 4, true>;
+        case 8: return k_sc_bin<16, 1, 2, true>;
+        case 9: return k_sc_bin<16, 4, 2, true>;
+        case 10: return k_sc_bin<32, 1, 1, true>;
+        case 11: return k_sc_bin<32, 2, 1, true>;
+        case 12: return k_sc_bin<16, 2, 2, true>;
+        default: return k_sc_bin<16, 1, 2, false>;
     }
 }
 
@@ -83,7 +95,8 @@ DevInfo dev_info() {
     if (hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return DevInfo{};
     for (int v = 0; v < kNumVariants; ++v) {
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, variant_kernel(v), kBlock, 0) != hipSuccess || occ < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, variant_kernel(v), kBlock, lds_bytes(v)) != hipSuccess ||
+            occ < 1)
             occ = 1;
         d.occ[v] = occ;
     }
@@ -125,7 +138,7 @@ extern "C" int pcub_sc_variant_info(int v, int* S, int* G, int* W) {
     if (v < 0 || v >= kNumVariants) return PCUB_EINVAL;
     *S = kVar[v].S;
     *G = kVar[v].G;
-    *W = kVar[v].W;
+    *W = kVar[v].W * (kVar[v].L ? -1 : 1);  // negative: deepest stage level in LDS
     return 0;
 }
 extern "C" int pcub_sc_set_variant(int v) {
@@ -185,6 +198,6 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
     A.nslots = nslots;
     A.scratch = (double2*)workspace;
     A.ybits = (uint32_t*)((char*)workspace + (size_t)nslots * (Nv / 2 - kVar[v].S) * sizeof(double2));
-    hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), 0, st, A);
+    hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), lds_bytes(v), st, A);
     return (int)hipGetLastError();
 }

@@ -101,87 +101,180 @@ struct SubV {
     }
 };
 
-// op from a level held in scratch (compact values), two outputs per pair.
-// Outputs pairs [0, Po) of depth d from the node at depth d-1 (2*Po pairs).
-template <bool G_OP>
-PCUB_HD void level_from_scratch(const double2* src, double2* dst, long long ns, int Po, const uint32_t* ybase) {
-#pragma unroll 2
-    for (int jp = 0; jp < Po; ++jp) {
-        const double2 a = src[(long long)jp * ns];
-        const double2 b = src[(long long)(jp + Po) * ns];
-        double2 o;
-        if (G_OP) {
-            const uint32_t w = ybase[(long long)(jp >> 4) * ns];
-            const uint32_t sh = (uint32_t)(2 * jp) & 31u;
-            o.x = op_g(a.x, b.x, (w >> sh) & 1u);
-            o.y = op_g(a.y, b.y, (w >> (sh + 1)) & 1u);
-        } else {
-            o.x = op_f(a.x, b.x);
-            o.y = op_f(a.y, b.y);
-        }
-        dst[(long long)jp * ns] = o;
-    }
+// One stored level of compact values: pair q (positions 2q, 2q+1) at p[q * s].
+struct Lvl {
+    double2* p;
+    long long s;
+};
+
+// Source of a fused chain pass: the raw root (depth 0) or a stored level, plus
+// the partial sums of the first op's minus child when that op is a plus transform.
+struct Chain {
+    const double2* in;  // root: this lane's row 2*bitrev_{nv-1}(t) at in[2*bitrev(t)*B] (lane part folded in)
+    long long B;
+    int nv;             // log2 of the virtual (per-lane) length
+    Lvl src;            // compact source level (depth a > 0)
+    const uint32_t* Y;  // local re-encoded bits, word w at Y[w * ns]
+    long long ns;
+    int ystart;         // first local u position of the minus child at depth a+1
+};
+
+// Root rows.  Local position t of lane j is real position p = j + G*t < N/2,
+// which pairs natural rows (2q, 2q+1) with q = bitrev_{n-1}(p).  The bits of j
+// and of G*t are disjoint, so q = bitrev_{n-1}(j) + bitrev_{nv-1}(t): the lane
+// part is folded into the lane's root pointer (Chain::in) once, and the row
+// offset of a position is wave-uniform.
+PCUB_HD long long root_row(int t, int nv) { return (long long)bitrev((uint32_t)t, nv - 1); }
+
+// Makes a per-lane pointer opaque to the optimiser at this point, so addresses
+// derived from it are recomputed in the loop (one or two VALU ops) instead of
+// being hoisted out of it and held live in registers across the whole schedule.
+template <class T>
+PCUB_HD T* launder(T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(p));
+#endif
+    return p;
 }
 
-// Natural row pair of the root at local position t of lane j: real position
-// p = j + G*t < N/2 pairs rows (2q, 2q+1) with q = bitrev_{n-1}(p).
-template <int G>
-PCUB_HD long long root_pair(int j, int t, int n) {
-    return (long long)bitrev((uint32_t)(j + G * t), n - 1);
+// Keeps the scheduler from hoisting the next column's loads above this point
+// (bounds the live registers of the unrolled final pass).
+PCUB_HD void sched_fence() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 
-// op from the raw root (depth 0).  For even t, p + G sets bit g of p, so
-// q(t+1) = q(t) + N/(4G).
-template <bool G_OP, int G>
-PCUB_HD void level_from_root(const double2* in, long long B, int n, int j, double2* dst, long long ns,
-                             const uint32_t* ybase) {
-    const int Po = (1 << (n - 2)) / G;  // N/(4G) output pairs
-    const long long step = (1LL << (n - 2)) / G;
-#pragma unroll 2
-    for (int jp = 0; jp < Po; ++jp) {
-        const int t = 2 * jp;
-        const long long p0 = root_pair<G>(j, t, n);
-        const long long p1 = p0 + step;
-        const double2 a0 = in[(2 * p0) * B], b0 = in[(2 * p0 + 1) * B];
-        const double2 a1 = in[(2 * p1) * B], b1 = in[(2 * p1 + 1) * B];
-        double2 o;
-        if (G_OP) {
-            const uint32_t w = ybase[(long long)(t >> 5) * ns];
-            const uint32_t sh = (uint32_t)t & 31u;
-            o.x = op_g_raw(a0, b0, (w >> sh) & 1u);
-            o.y = op_g_raw(a1, b1, (w >> (sh + 1)) & 1u);
-        } else {
-            o.x = op_f_raw(a0, b0);
-            o.y = op_f_raw(a1, b1);
-        }
-        dst[(long long)jp * ns] = o;
-    }
-}
-
-// Final op into registers: v[t] = op(in[t], in[t+S]) for the depth D-1 node of 2S local values.
-template <int S, bool G_OP>
-PCUB_HD void final_from_scratch(const double2* src, long long ns, double* v, uint32_t ybits) {
+// Fused column pair.  From the depth-a node (La local values) evaluate F levels
+// for the two columns p, p+1 (p even) of stride C = La >> F: level a+e holds
+// positions p + m*C, m < 2^(F-e), and needs level a+e-1 at m and m + 2^(F-e).
+// The first op is a plus transform when FG (bits of the minus child), else a
+// minus transform; every later op is a minus transform (an SC chain descends
+// through minus children).  y receives levels a+1 .. a+F back to back
+// (2^(F-1), 2^(F-2), .., 1 entries; .x = column p, .y = column p+1).
+template <int F, bool FG, bool ROOT, int G>
+PCUB_HD void colpair(const Chain& c, int p, int C, double2* y) {
+    constexpr int H = 1 << (F - 1);
 #pragma unroll
-    for (int jp = 0; jp < S / 2; ++jp) {
-        const double2 a = src[(long long)jp * ns];
-        const double2 b = src[(long long)(jp + S / 2) * ns];
-        if (G_OP) {
-            v[2 * jp] = op_g(a.x, b.x, (ybits >> (2 * jp)) & 1u);
-            v[2 * jp + 1] = op_g(a.y, b.y, (ybits >> (2 * jp + 1)) & 1u);
+    for (int m = 0; m < H; ++m) {
+        const int P = p + m * C;
+        uint32_t u0 = 0, u1 = 0;
+        if (FG) {
+            const int bp = c.ystart + P;  // even: bits bp, bp+1 share a word
+            const uint32_t w = c.Y[(long long)(bp >> 5) * c.ns] >> (bp & 31);
+            u0 = w & 1u;
+            u1 = (w >> 1) & 1u;
+        }
+        double2 o;
+        if (ROOT) {
+            // positions P, P + Nv/2 are rows (2q, 2q+1); P+1 adds Nv/4 to q
+            const long long q0 = root_row(P, c.nv);
+            const long long q1 = q0 + (1LL << (c.nv - 2));
+            const double2 a0 = c.in[(2 * q0) * c.B], b0 = c.in[(2 * q0 + 1) * c.B];
+            const double2 a1 = c.in[(2 * q1) * c.B], b1 = c.in[(2 * q1 + 1) * c.B];
+            o.x = FG ? op_g_raw(a0, b0, u0) : op_f_raw(a0, b0);
+            o.y = FG ? op_g_raw(a1, b1, u1) : op_f_raw(a1, b1);
         } else {
-            v[2 * jp] = op_f(a.x, b.x);
-            v[2 * jp + 1] = op_f(a.y, b.y);
+            const double2 a = c.src.p[(long long)(P >> 1) * c.src.s];
+            const double2 b = c.src.p[(long long)((P + H * C) >> 1) * c.src.s];
+            o.x = FG ? op_g(a.x, b.x, u0) : op_f(a.x, b.x);
+            o.y = FG ? op_g(a.y, b.y, u1) : op_f(a.y, b.y);
+        }
+        y[m] = o;
+    }
+    int in_off = 0, out_off = H;
+#pragma unroll
+    for (int e = 2; e <= F; ++e) {
+        const int He = 1 << (F - e);
+#pragma unroll
+        for (int m = 0; m < He; ++m) {
+            y[out_off + m].x = op_f(y[in_off + m].x, y[in_off + m + He].x);
+            y[out_off + m].y = op_f(y[in_off + m].y, y[in_off + m + He].y);
+        }
+        in_off = out_off;
+        out_off += He;
+    }
+}
+
+// Where stored level d (1 <= d <= D-1) lives: the per-slot scratch, or `last` for d == D-1.
+struct LevelMap {
+    double2* scr;
+    long long ns;
+    int Nv;
+    int D;
+    Lvl last;
+    PCUB_HD Lvl get(int d) const {
+        if (last.p && d == D - 1) return last;
+        return Lvl{scr + (long long)(Nv / 2 - (Nv >> d)) * ns, ns};
+    }
+};
+
+// Non-final pass: levels a+1 .. a+F are all stored.
+template <int F, bool FG, bool ROOT, int G>
+PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
+    Lvl lv[F];
+#pragma unroll
+    for (int e = 1; e <= F; ++e) lv[e - 1] = lm.get(a + e);
+    const int C = La >> F;
+#pragma unroll 1
+    for (int p = 0; p < C; p += 2) {
+        double2 y[(1 << F) - 1];
+        colpair<F, FG, ROOT, G>(c, p, C, y);
+        int off = 0;
+#pragma unroll
+        for (int e = 1; e <= F; ++e) {
+            const int He = 1 << (F - e);
+#pragma unroll
+            for (int m = 0; m < He; ++m) lv[e - 1].p[(long long)((p + m * C) >> 1) * lv[e - 1].s] = y[off + m];
+            off += He;
         }
     }
 }
 
-template <int S, bool G_OP, int G>
-PCUB_HD void final_from_root(const double2* in, long long B, int n, int j, double* v, uint32_t ybits) {
+// Final pass into registers (F = 1 or 2): with F = 2, level D-1 is stored to
+// `l1`; level D (S values) goes into v.  Level D-1 is touched only here (as
+// l1, or as c.src when F = 1), which lets it live in LDS with static addressing.
+template <int S, int F, bool FG, bool ROOT, int G>
+PCUB_HD void chain_final(const Chain& c, Lvl l1, double* v) {
+    static_assert(F == 1 || F == 2, "final pass fuses at most two levels");
+    const Lvl lv[1] = {l1};
 #pragma unroll
-    for (int t = 0; t < S; ++t) {
-        const long long p = root_pair<G>(j, t, n);
-        const double2 a = in[(2 * p) * B], b = in[(2 * p + 1) * B];
-        v[t] = G_OP ? op_g_raw(a, b, (ybits >> t) & 1u) : op_f_raw(a, b);
+    for (int p = 0; p < S; p += 2) {
+        double2 y[(1 << F) - 1];
+        colpair<F, FG, ROOT, G>(c, p, S, y);
+        int off = 0;
+#pragma unroll
+        for (int e = 1; e < F; ++e) {
+            const int He = 1 << (F - e);
+#pragma unroll
+            for (int m = 0; m < He; ++m) lv[e - 1].p[(long long)((p + m * S) >> 1) * lv[e - 1].s] = y[off + m];
+            off += He;
+        }
+        v[p] = y[(1 << F) - 2].x;
+        v[p + 1] = y[(1 << F) - 2].y;
+        sched_fence();
+    }
+}
+
+template <int F, int G>
+PCUB_HD void dispatch_pass(const Chain& c, int La, const LevelMap& lm, int a, bool fg, bool root) {
+    if (root) {
+        if (fg) chain_pass<F, true, true, G>(c, La, lm, a);
+        else chain_pass<F, false, true, G>(c, La, lm, a);
+    } else {
+        if (fg) chain_pass<F, true, false, G>(c, La, lm, a);
+        else chain_pass<F, false, false, G>(c, La, lm, a);
+    }
+}
+
+template <int S, int F, int G>
+PCUB_HD void dispatch_final(const Chain& c, Lvl l1, double* v, bool fg, bool root) {
+    if (root) {
+        if (fg) chain_final<S, F, true, true, G>(c, l1, v);
+        else chain_final<S, F, false, true, G>(c, l1, v);
+    } else {
+        if (fg) chain_final<S, F, true, false, G>(c, l1, v);
+        else chain_final<S, F, false, false, G>(c, l1, v);
     }
 }
 
@@ -189,8 +282,9 @@ PCUB_HD void final_from_root(const double2* in, long long B, int n, int j, doubl
 // G lanes (`lane` = wave lane id, for the exchanges) in scratch slot `slot`.
 // S = virtual register subtree (values per lane) in {8, 16, 32}; requires
 // N >= 2*S*G and N >= 32*G.  `store` is false for padding codewords.
-template <int S, int G>
-PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store) {
+template <int S, int G, bool LDS = false>
+PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
+                             Lvl last = Lvl{nullptr, 0}) {
     static_assert(S == 8 || S == 16 || S == 32, "register subtree must fit one Y word");
     static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lanes per codeword");
     constexpr int s = (S == 8) ? 3 : (S == 16) ? 4 : 5;
@@ -205,45 +299,69 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     const int D = nv - s;
     const long long ns = A.nslots;
     const long long B = A.B;
-    const double2* in = A.xy + cw;
+    const double2* in = A.xy + cw + 2 * (long long)bitrev((uint32_t)j, n - 1) * B;
     double2* scr = A.scratch + slot;
     uint32_t* Y = A.ybits + slot;
+
+    // stored levels 1 .. D-2 in the slot scratch; level D-1 there too, or in LDS (`last`)
+    LevelMap lm;
+    lm.scr = scr;
+    lm.ns = ns;
+    lm.Nv = Nv;
+    lm.D = D;
+    lm.last = Lvl{nullptr, 0};
+    Lvl lastlv;
+    if constexpr (LDS) lastlv = last;
+    else lastlv = lm.get(D - 1);
 
     uint64_t acc = 0;
     int nacc = 0;
     int infow = 0;
 
     for (int k = 0; k < (1 << D); ++k) {
+        in = launder(in);
+        scr = launder(scr);
+        Y = launder(Y);
+        lm.scr = scr;
+        if constexpr (!LDS) lastlv = lm.get(D - 1);
+        // The chain for subtree k: a plus transform at depth d0-1 (minus for k == 0)
+        // then minus transforms down to depth D.  Passes of up to 3 fused levels;
+        // the last pass (1 or 2 levels) ends in registers.  Only a pass's source
+        // level is read from memory: every level written inside a chain is
+        // consumed from registers by the next transform.
         const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
-        // depths d0 .. D-1 into scratch
-        for (int d = d0; d < D; ++d) {
-            const bool gop = (d == d0) && (k != 0);
-            const int Po = Nv >> (d + 1);  // output pairs at depth d
-            double2* dst = scr + (long long)(Nv / 2 - (Nv >> d)) * ns;
-            // minus child of the depth d-1 node: local u range starts at (k >> (D-d+1)) * (Nv >> (d-1))
-            const uint32_t* yb = Y + (long long)(((k >> (D - d + 1)) << (nv - d + 1)) >> 5) * ns;
-            if (d == 1) {
-                if (gop) level_from_root<true, G>(in, B, n, j, dst, ns, yb);
-                else level_from_root<false, G>(in, B, n, j, dst, ns, yb);
-            } else {
-                const double2* src = scr + (long long)(Nv / 2 - (Nv >> (d - 1))) * ns;
-                if (gop) level_from_scratch<true>(src, dst, ns, Po, yb);
-                else level_from_scratch<false>(src, dst, ns, Po, yb);
-            }
+        int a = d0 - 1;
+        bool fg = (k != 0);
+        int T = D - a;
+        const int Ffin = T >= 2 ? 2 : 1;
+        Chain c;
+        c.in = in;
+        c.B = B;
+        c.nv = nv;
+        c.Y = Y;
+        c.ns = ns;
+        while (T > Ffin) {
+            const int F = (T - Ffin) >= 3 ? 3 : (T - Ffin);
+            c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
+            c.ystart = (k >> (D - a)) << (nv - a);
+            const int La = Nv >> a;
+            if (F == 3) dispatch_pass<3, G>(c, La, lm, a, fg, a == 0);
+            else if (F == 2) dispatch_pass<2, G>(c, La, lm, a, fg, a == 0);
+            else dispatch_pass<1, G>(c, La, lm, a, fg, a == 0);
+            a += F;
+            T -= F;
+            fg = false;
         }
-        // depth D into registers.  The minus child of the depth D-1 node starts
-        // at local bit (k>>1)*2S.
         double v[S];
-        const bool gD = (d0 == D) && (k != 0);
-        const int mstart = (k >> 1) * 2 * S;
-        const uint32_t ybD = gD ? (Y[(long long)(mstart >> 5) * ns] >> (mstart & 31)) : 0u;
-        if (D == 1) {
-            if (gD) final_from_root<S, true, G>(in, B, n, j, v, ybD);
-            else final_from_root<S, false, G>(in, B, n, j, v, ybD);
+        c.ystart = (k >> (D - a)) << (nv - a);
+        if (Ffin == 2) {
+            c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
+            dispatch_final<S, 2, G>(c, lastlv, v, fg, a == 0);
+        } else if (a > 0) {
+            c.src = lastlv;
+            dispatch_final<S, 1, G>(c, lastlv, v, fg, false);
         } else {
-            const double2* src = scr + (long long)(Nv / 2 - (Nv >> (D - 1))) * ns;
-            if (gD) final_from_scratch<S, true>(src, ns, v, ybD);
-            else final_from_scratch<S, false>(src, ns, v, ybD);
+            dispatch_final<S, 1, G>(c, lastlv, v, fg, true);
         }
         // frozen bits of real u range [k*SU, (k+1)*SU)
         const int ustart = k * SU;

@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--ebn0", type=float, default=2.0)
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU")
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--max-blocks", type=int, default=0, help="cap decode workgroups per CU (0 = occupancy)")
     ap.add_argument("--seed", type=int, default=20250204)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-xhat", action="store_true")
@@ -118,6 +119,7 @@ def main():
     frozen = construction.bhattacharyya_frozen(n, K, sigma2)
     code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(frozen)[0].tolist()), 1, device=device)
     sc.set_variant(args.variant)
+    sc.set_max_blocks_per_cu(args.max_blocks)
     dec = sc.BinaryDecoder(code)
     B = args.batch
 
@@ -182,7 +184,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic: uniform info bits, GPU polar encoder, BI-AWGN Eb/N0=%.1f dB pairs generated on device" % args.ebn0,
             "config": {"workload": "binary SC decode N=%d K=%d BI-AWGN %.1f dB (BASELINE configs[1])" % (N, K, args.ebn0),
-                       "N": N, "K": K, "batch_per_gpu": B, "ebn0_db": args.ebn0, "kernel_variant": args.variant,
+                       "N": N, "K": K, "batch_per_gpu": B, "ebn0_db": args.ebn0, "kernel_variant": args.variant, "max_blocks_per_cu": args.max_blocks,
                        "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world},
             "fer": float(counters[1].item()) / int(counters[0].item()),
             "frame_errors": int(counters[1].item()),

@@ -24,21 +24,24 @@ constexpr int kBlock = 256;
 
 // Decode kernel variants: virtual register subtree S (values per lane), lanes
 // per codeword G, and the minimum waves/SIMD the register allocation must allow.
-// LDS: the deepest stage level (depth D-1, 2S values per lane) lives in LDS.
+// Variant fields: S = register subtree values per lane, G = lanes per codeword,
+// W = minimum waves/SIMD for register allocation, L = deepest stage level in
+// LDS, T = non-temporal loads for the (once-streamed) input rows.
 struct Variant {
-    int S, G, W, L;
+    int S, G, W, L, T;
 };
-constexpr int kNumVariants = 13;
+constexpr int kNumVariants = 15;
 constexpr Variant kVar[kNumVariants] = {
-    {16, 1, 2, 0}, {8, 1, 4, 0}, {32, 1, 1, 0}, {16, 4, 2, 0}, {8, 4, 4, 0}, {16, 2, 2, 0}, {32, 2, 1, 0},
-    {8, 4, 4, 1},  {16, 1, 2, 1}, {16, 4, 2, 1}, {32, 1, 1, 1}, {32, 2, 1, 1}, {16, 2, 2, 1},
+    {16, 1, 2, 0, 0}, {8, 1, 4, 0, 0}, {32, 1, 1, 0, 0}, {16, 4, 2, 0, 0}, {8, 4, 4, 0, 0}, {16, 2, 2, 0, 0},
+    {32, 2, 1, 0, 0}, {8, 8, 4, 0, 0}, {16, 2, 2, 0, 1}, {8, 8, 4, 0, 1}, {16, 4, 2, 0, 1}, {8, 4, 4, 1, 0},
+    {16, 2, 2, 0, 2}, {16, 4, 2, 0, 2}, {8, 4, 4, 0, 2},
 };
 
 size_t lds_bytes(int v) { return kVar[v].L ? (size_t)kVar[v].S * kBlock * sizeof(double2) : 0; }
 
-template <int S, int G, int W, bool LDS>
+template <int S, int G, int W, bool LDS, int NT>
 __global__ __launch_bounds__(kBlock, W) void k_sc_bin(BinArgs A) {
-    extern __shared__ double2 lds_last[];  // [S pairs][kBlock] when LDS
+    extern __shared__ double2 lds_last[];  // [S pairs][kBlock] when LDS (plus occupancy padding)
     constexpr int CWB = kBlock / G;  // codewords per workgroup tile
     const long long slot = (long long)blockIdx.x * kBlock + threadIdx.x;
     const int j = threadIdx.x & (G - 1);
@@ -48,7 +51,7 @@ __global__ __launch_bounds__(kBlock, W) void k_sc_bin(BinArgs A) {
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_codeword<S, G, LDS>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last);
+        decode_codeword<S, G, LDS, NT>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last);
     }
 }
 
@@ -61,23 +64,37 @@ __global__ __launch_bounds__(kBlock) void k_sc_bin_small(BinArgs A) {
 typedef void (*KernFn)(BinArgs);
 KernFn variant_kernel(int v) {
     switch (v) {
-        case 1: return k_sc_bin<8, 1, 4, false>;
-        case 2: return k_sc_bin<32, 1, 1, false>;
-        case 3: return k_sc_bin<16, 4, 2, false>;
-        case 4: return k_sc_bin<8, 4, 4, false>;
-        case 5: return k_sc_bin<16, 2, 2, false>;
-        case 6: return k_sc_bin<32, 2, 1, false>;
-        case 7: return k_sc_bin<8, 4, 4, true>;
-        case 8: return k_sc_bin<16, 1, 2, true>;
-        case 9: return k_sc_bin<16, 4, 2, true>;
-        case 10: return k_sc_bin<32, 1, 1, true>;
-        case 11: return k_sc_bin<32, 2, 1, true>;
-        case 12: return k_sc_bin<16, 2, 2, true>;
-        default: return k_sc_bin<16, 1, 2, false>;
+        case 1: return k_sc_bin<8, 1, 4, false, 0>;
+        case 2: return k_sc_bin<32, 1, 1, false, 0>;
+        case 3: return k_sc_bin<16, 4, 2, false, 0>;
+        case 4: return k_sc_bin<8, 4, 4, false, 0>;
+        case 5: return k_sc_bin<16, 2, 2, false, 0>;
+        case 6: return k_sc_bin<32, 2, 1, false, 0>;
+        case 7: return k_sc_bin<8, 8, 4, false, 0>;
+        case 8: return k_sc_bin<16, 2, 2, false, 1>;
+        case 9: return k_sc_bin<8, 8, 4, false, 1>;
+        case 10: return k_sc_bin<16, 4, 2, false, 1>;
+        case 11: return k_sc_bin<8, 4, 4, true, 0>;
+        case 12: return k_sc_bin<16, 2, 2, false, 2>;
+        case 13: return k_sc_bin<16, 4, 2, false, 2>;
+        case 14: return k_sc_bin<8, 4, 4, false, 2>;
+        default: return k_sc_bin<16, 1, 2, false, 0>;
     }
 }
 
 int g_variant = 0;
+int g_max_blocks = 0;  // workgroups per CU cap (0 = as many as fit)
+constexpr size_t kLdsPerCu = 160 * 1024;
+
+// dynamic LDS for variant v: its stage level plus padding that caps residency at g_max_blocks
+size_t launch_lds(int v) {
+    size_t b = lds_bytes(v);
+    if (g_max_blocks > 0) {
+        const size_t cap = kLdsPerCu / (size_t)g_max_blocks;
+        if (cap > b) b = cap - 256;
+    }
+    return b;
+}
 
 struct DevInfo {
     int dev = -1;
@@ -115,7 +132,9 @@ long long grid_for(long long B, int v) {
     if (d.cus <= 0) return 0;
     const long long cwb = kBlock / kVar[v].G;
     const long long ntiles = (B + cwb - 1) / cwb;
-    long long g = (long long)d.cus * d.occ[v];
+    int occ = d.occ[v];
+    if (g_max_blocks > 0 && g_max_blocks < occ) occ = g_max_blocks;
+    long long g = (long long)d.cus * occ;
     return ntiles < g ? ntiles : g;
 }
 
@@ -141,6 +160,12 @@ extern "C" int pcub_sc_variant_info(int v, int* S, int* G, int* W) {
     *W = kVar[v].W * (kVar[v].L ? -1 : 1);  // negative: deepest stage level in LDS
     return 0;
 }
+extern "C" int pcub_sc_set_max_blocks_per_cu(int b) {
+    if (b < 0 || b > 8) return PCUB_EINVAL;
+    g_max_blocks = b;
+    return 0;
+}
+
 extern "C" int pcub_sc_set_variant(int v) {
     if (v < 0 || v >= kNumVariants) return PCUB_EINVAL;
     g_variant = v;
@@ -198,6 +223,6 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
     A.nslots = nslots;
     A.scratch = (double2*)workspace;
     A.ybits = (uint32_t*)((char*)workspace + (size_t)nslots * (Nv / 2 - kVar[v].S) * sizeof(double2));
-    hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), lds_bytes(v), st, A);
+    hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), launch_lds(v), st, A);
     return (int)hipGetLastError();
 }

@@ -119,6 +119,61 @@ struct Chain {
     int ystart;         // first local u position of the minus child at depth a+1
 };
 
+// Global-memory access helpers.  The per-k pointer laundering (see launder())
+// hides the pointers' provenance, so without an explicit address-space cast the
+// compiler emits flat instructions (which also tie up the LDS counter).  GL =
+// false keeps a generic access (for a level that may live in LDS).  NT = non-
+// temporal: the input rows are streamed exactly twice, far apart in time.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) d2v gd2v;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+#endif
+
+template <bool NT = false, bool GL = true>
+PCUB_HD double2 ld2(const double2* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (GL) {
+        const gd2v* g = (const gd2v*)p;
+        const d2v v = NT ? __builtin_nontemporal_load(g) : *g;
+        return double2{v.x, v.y};
+    }
+#endif
+    return *p;
+}
+
+template <bool NT = false, bool GL = true>
+PCUB_HD void st2(double2* p, double2 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (GL) {
+        gd2v* g = (gd2v*)p;
+        d2v t;
+        t.x = v.x;
+        t.y = v.y;
+        if constexpr (NT) __builtin_nontemporal_store(t, g);
+        else *g = t;
+        return;
+    }
+#endif
+    *p = v;
+}
+
+PCUB_HD uint32_t ldu(const uint32_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const gu32*)p;
+#else
+    return *p;
+#endif
+}
+
+PCUB_HD void stu(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *(gu32*)p = v;
+#else
+    *p = v;
+#endif
+}
+
 // Root rows.  Local position t of lane j is real position p = j + G*t < N/2,
 // which pairs natural rows (2q, 2q+1) with q = bitrev_{n-1}(p).  The bits of j
 // and of G*t are disjoint, so q = bitrev_{n-1}(j) + bitrev_{nv-1}(t): the lane
@@ -152,8 +207,9 @@ PCUB_HD void sched_fence() {
 // minus transform; every later op is a minus transform (an SC chain descends
 // through minus children).  y receives levels a+1 .. a+F back to back
 // (2^(F-1), 2^(F-2), .., 1 entries; .x = column p, .y = column p+1).
-template <int F, bool FG, bool ROOT, int G>
+template <int F, bool FG, int R, int G, bool NS = false, bool GL = true>
 PCUB_HD void colpair(const Chain& c, int p, int C, double2* y) {
+    constexpr bool ROOT = R != 0;
     constexpr int H = 1 << (F - 1);
 #pragma unroll
     for (int m = 0; m < H; ++m) {
@@ -161,7 +217,7 @@ PCUB_HD void colpair(const Chain& c, int p, int C, double2* y) {
         uint32_t u0 = 0, u1 = 0;
         if (FG) {
             const int bp = c.ystart + P;  // even: bits bp, bp+1 share a word
-            const uint32_t w = c.Y[(long long)(bp >> 5) * c.ns] >> (bp & 31);
+            const uint32_t w = ldu(c.Y + (long long)(bp >> 5) * c.ns) >> (bp & 31);
             u0 = w & 1u;
             u1 = (w >> 1) & 1u;
         }
@@ -170,13 +226,15 @@ PCUB_HD void colpair(const Chain& c, int p, int C, double2* y) {
             // positions P, P + Nv/2 are rows (2q, 2q+1); P+1 adds Nv/4 to q
             const long long q0 = root_row(P, c.nv);
             const long long q1 = q0 + (1LL << (c.nv - 2));
-            const double2 a0 = c.in[(2 * q0) * c.B], b0 = c.in[(2 * q0 + 1) * c.B];
-            const double2 a1 = c.in[(2 * q1) * c.B], b1 = c.in[(2 * q1 + 1) * c.B];
+            const double2 a0 = ld2<R == 2>(c.in + (2 * q0) * c.B);
+            const double2 b0 = ld2<R == 2>(c.in + (2 * q0 + 1) * c.B);
+            const double2 a1 = ld2<R == 2>(c.in + (2 * q1) * c.B);
+            const double2 b1 = ld2<R == 2>(c.in + (2 * q1 + 1) * c.B);
             o.x = FG ? op_g_raw(a0, b0, u0) : op_f_raw(a0, b0);
             o.y = FG ? op_g_raw(a1, b1, u1) : op_f_raw(a1, b1);
         } else {
-            const double2 a = c.src.p[(long long)(P >> 1) * c.src.s];
-            const double2 b = c.src.p[(long long)((P + H * C) >> 1) * c.src.s];
+            const double2 a = ld2<NS, GL>(c.src.p + (long long)(P >> 1) * c.src.s);
+            const double2 b = ld2<NS, GL>(c.src.p + (long long)((P + H * C) >> 1) * c.src.s);
             o.x = FG ? op_g(a.x, b.x, u0) : op_f(a.x, b.x);
             o.y = FG ? op_g(a.y, b.y, u1) : op_f(a.y, b.y);
         }
@@ -210,7 +268,7 @@ struct LevelMap {
 };
 
 // Non-final pass: levels a+1 .. a+F are all stored.
-template <int F, bool FG, bool ROOT, int G>
+template <int F, bool FG, int R, int G, bool NS>
 PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
     Lvl lv[F];
 #pragma unroll
@@ -219,13 +277,13 @@ PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
 #pragma unroll 1
     for (int p = 0; p < C; p += 2) {
         double2 y[(1 << F) - 1];
-        colpair<F, FG, ROOT, G>(c, p, C, y);
+        colpair<F, FG, R, G, NS>(c, p, C, y);
         int off = 0;
 #pragma unroll
         for (int e = 1; e <= F; ++e) {
             const int He = 1 << (F - e);
 #pragma unroll
-            for (int m = 0; m < He; ++m) lv[e - 1].p[(long long)((p + m * C) >> 1) * lv[e - 1].s] = y[off + m];
+            for (int m = 0; m < He; ++m) st2<NS>(lv[e - 1].p + (long long)((p + m * C) >> 1) * lv[e - 1].s, y[off + m]);
             off += He;
         }
     }
@@ -234,20 +292,20 @@ PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
 // Final pass into registers (F = 1 or 2): with F = 2, level D-1 is stored to
 // `l1`; level D (S values) goes into v.  Level D-1 is touched only here (as
 // l1, or as c.src when F = 1), which lets it live in LDS with static addressing.
-template <int S, int F, bool FG, bool ROOT, int G>
+template <int S, int F, bool FG, int R, int G, bool NS, bool LL>
 PCUB_HD void chain_final(const Chain& c, Lvl l1, double* v) {
     static_assert(F == 1 || F == 2, "final pass fuses at most two levels");
     const Lvl lv[1] = {l1};
 #pragma unroll
     for (int p = 0; p < S; p += 2) {
         double2 y[(1 << F) - 1];
-        colpair<F, FG, ROOT, G>(c, p, S, y);
+        colpair<F, FG, R, G, NS && F == 2, F == 2 || !LL>(c, p, S, y);
         int off = 0;
 #pragma unroll
         for (int e = 1; e < F; ++e) {
             const int He = 1 << (F - e);
 #pragma unroll
-            for (int m = 0; m < He; ++m) lv[e - 1].p[(long long)((p + m * S) >> 1) * lv[e - 1].s] = y[off + m];
+            for (int m = 0; m < He; ++m) st2<false, !LL>(lv[e - 1].p + (long long)((p + m * S) >> 1) * lv[e - 1].s, y[off + m]);
             off += He;
         }
         v[p] = y[(1 << F) - 2].x;
@@ -256,25 +314,27 @@ PCUB_HD void chain_final(const Chain& c, Lvl l1, double* v) {
     }
 }
 
-template <int F, int G>
+// root: 0 = compact source level, RR = root (1 plain, 2 non-temporal loads)
+// NS: non-temporal access to the upper stage levels (all but level D-1)
+template <int F, int G, int RR, bool NS>
 PCUB_HD void dispatch_pass(const Chain& c, int La, const LevelMap& lm, int a, bool fg, bool root) {
     if (root) {
-        if (fg) chain_pass<F, true, true, G>(c, La, lm, a);
-        else chain_pass<F, false, true, G>(c, La, lm, a);
+        if (fg) chain_pass<F, true, RR, G, NS>(c, La, lm, a);
+        else chain_pass<F, false, RR, G, NS>(c, La, lm, a);
     } else {
-        if (fg) chain_pass<F, true, false, G>(c, La, lm, a);
-        else chain_pass<F, false, false, G>(c, La, lm, a);
+        if (fg) chain_pass<F, true, 0, G, NS>(c, La, lm, a);
+        else chain_pass<F, false, 0, G, NS>(c, La, lm, a);
     }
 }
 
-template <int S, int F, int G>
+template <int S, int F, int G, int RR, bool NS, bool LL>
 PCUB_HD void dispatch_final(const Chain& c, Lvl l1, double* v, bool fg, bool root) {
     if (root) {
-        if (fg) chain_final<S, F, true, true, G>(c, l1, v);
-        else chain_final<S, F, false, true, G>(c, l1, v);
+        if (fg) chain_final<S, F, true, RR, G, NS, LL>(c, l1, v);
+        else chain_final<S, F, false, RR, G, NS, LL>(c, l1, v);
     } else {
-        if (fg) chain_final<S, F, true, false, G>(c, l1, v);
-        else chain_final<S, F, false, false, G>(c, l1, v);
+        if (fg) chain_final<S, F, true, 0, G, NS, LL>(c, l1, v);
+        else chain_final<S, F, false, 0, G, NS, LL>(c, l1, v);
     }
 }
 
@@ -282,7 +342,8 @@ PCUB_HD void dispatch_final(const Chain& c, Lvl l1, double* v, bool fg, bool roo
 // G lanes (`lane` = wave lane id, for the exchanges) in scratch slot `slot`.
 // S = virtual register subtree (values per lane) in {8, 16, 32}; requires
 // N >= 2*S*G and N >= 32*G.  `store` is false for padding codewords.
-template <int S, int G, bool LDS = false>
+// NT: 0 = cached loads/stores, 1 = non-temporal input rows, 2 = also the upper stage levels
+template <int S, int G, bool LDS = false, int NT = 0>
 PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
                              Lvl last = Lvl{nullptr, 0}) {
     static_assert(S == 8 || S == 16 || S == 32, "register subtree must fit one Y word");
@@ -293,6 +354,8 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     constexpr int SU = S * G;  // real u positions per register subtree (<= 64)
     static_assert(SU <= 64, "u decisions of one subtree must fit 64 bits");
     constexpr uint64_t SUMASK = (SU == 64) ? ~0ull : ((1ull << SU) - 1ull);
+    constexpr int RR = NT >= 1 ? 2 : 1;
+    constexpr bool NS = NT >= 2;
     const int n = A.n;
     const int nv = n - g;
     const int Nv = 1 << nv;
@@ -345,9 +408,9 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
             c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
             c.ystart = (k >> (D - a)) << (nv - a);
             const int La = Nv >> a;
-            if (F == 3) dispatch_pass<3, G>(c, La, lm, a, fg, a == 0);
-            else if (F == 2) dispatch_pass<2, G>(c, La, lm, a, fg, a == 0);
-            else dispatch_pass<1, G>(c, La, lm, a, fg, a == 0);
+            if (F == 3) dispatch_pass<3, G, RR, NS>(c, La, lm, a, fg, a == 0);
+            else if (F == 2) dispatch_pass<2, G, RR, NS>(c, La, lm, a, fg, a == 0);
+            else dispatch_pass<1, G, RR, NS>(c, La, lm, a, fg, a == 0);
             a += F;
             T -= F;
             fg = false;
@@ -356,12 +419,12 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         c.ystart = (k >> (D - a)) << (nv - a);
         if (Ffin == 2) {
             c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
-            dispatch_final<S, 2, G>(c, lastlv, v, fg, a == 0);
+            dispatch_final<S, 2, G, RR, NS, LDS>(c, lastlv, v, fg, a == 0);
         } else if (a > 0) {
             c.src = lastlv;
-            dispatch_final<S, 1, G>(c, lastlv, v, fg, false);
+            dispatch_final<S, 1, G, RR, NS, LDS>(c, lastlv, v, fg, false);
         } else {
-            dispatch_final<S, 1, G>(c, lastlv, v, fg, true);
+            dispatch_final<S, 1, G, RR, NS, LDS>(c, lastlv, v, fg, true);
         }
         // frozen bits of real u range [k*SU, (k+1)*SU)
         const int ustart = k * SU;
@@ -379,8 +442,8 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         // local encoding bits of virtual subtree k
         const int lstart = k * S;
         uint32_t* yw = Y + (long long)(lstart >> 5) * ns;
-        if (S == 32) *yw = y;
-        else *yw = ((lstart & 31) == 0 ? 0u : (*yw & ((1u << (lstart & 31)) - 1u))) | (y << (lstart & 31));
+        if (S == 32) stu(yw, y);
+        else stu(yw, ((lstart & 31) == 0 ? 0u : (ldu(yw) & ((1u << (lstart & 31)) - 1u))) | (y << (lstart & 31)));
         if (A.uout && store && j == 0) {
             uint32_t* uo = A.uout + (long long)uw * B + cw;
             if constexpr (SU == 64) {
@@ -409,14 +472,16 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
             if (Lc < 32) {  // parent fits in one word (S < 32, deepest levels)
                 const int pstart = (k >> (D - d + 1)) * 2 * Lc;
                 uint32_t* pw = Y + (long long)(pstart >> 5) * ns;
-                const uint32_t w = *pw >> (pstart & 31);
+                const uint32_t w0 = ldu(pw);
+                const uint32_t w = w0 >> (pstart & 31);
                 const uint32_t lm = (1u << Lc) - 1u;
-                *pw ^= ((w >> Lc) & lm) << (pstart & 31);
+                stu(pw, w0 ^ (((w >> Lc) & lm) << (pstart & 31)));
                 continue;
             }
             const int Wc = Lc >> 5;
             uint32_t* base = Y + (long long)((k >> (D - d + 1)) * (2 * Wc)) * ns;
-            for (int w = 0; w < Wc; ++w) base[(long long)w * ns] ^= base[(long long)(w + Wc) * ns];
+            for (int w = 0; w < Wc; ++w)
+                stu(base + (long long)w * ns, ldu(base + (long long)w * ns) ^ ldu(base + (long long)(w + Wc) * ns));
         }
     }
     if (nacc && store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
@@ -428,7 +493,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
             uint32_t o = 0;
             for (int t = 0; t < 32; ++t) {
                 const uint32_t p = bitrev((uint32_t)(32 * w + t), nv);
-                o |= ((Y[(long long)(p >> 5) * ns] >> (p & 31u)) & 1u) << t;
+                o |= ((ldu(Y + (long long)(p >> 5) * ns) >> (p & 31u)) & 1u) << t;
             }
             A.xhat[(long long)(seg * W + w) * B + cw] = o;
         }

@@ -8,8 +8,16 @@
 // (0, 0).  We store it in ONE binary64:
 //     +r   <=> (1, r)
 //     -r   <=> (r, 1)        (-0.0 encodes (0, 1); the tie (1,1) may carry either sign)
-//     2.0  <=> (0, 0)        ("sentinel", any value > 1)
+//     NaN  <=> (0, 0)        (either sign)
 // x/x == 1 exactly for finite non-zero x, so the stored form loses nothing.
+// (0, 0) is absorbing in both transforms (every product in the output has a
+// factor from it), and NaN is absorbing in IEEE arithmetic, so the sentinel
+// needs no flag: a (0, 0) that arises inside a transform (0/0 in the
+// normalisation) is produced by the division itself, and every decision
+// below is a strict comparison, false on NaN, i.e. the reference's decision
+// 0 for an all-zero leaf.  No select below may become a min/max instruction
+// (those drop NaNs); they are written as compare + select and the library is
+// built without fast-math.
 //
 // Canonical arithmetic.  Swapping the two components of an input flips the
 // output of the minus transform (its two sums are the same rounded terms,
@@ -27,39 +35,34 @@
 
 namespace pcub {
 
-constexpr double kSentinel = 2.0;
 
 PCUB_HD long long as_bits(double v) { return __builtin_bit_cast(long long, v); }
 PCUB_HD double from_bits(long long b) { return __builtin_bit_cast(double, b); }
 
 struct CV {
-    double r;    // ratio in [0,1] (garbage when z)
+    double r;    // ratio in [0,1], NaN for (0, 0)
     uint32_t s;  // orientation: 1 <=> (r, 1)
-    bool z;      // (0, 0)
 };
 
 PCUB_HD CV cv_load(double v) {
     CV c;
     c.s = (uint32_t)((unsigned long long)as_bits(v) >> 63);
     c.r = __builtin_fabs(v);
-    c.z = c.r > 1.0;
     return c;
 }
 
-PCUB_HD double cv_pack(double q, uint32_t s, bool z) {
-    // q >= +0 always, so OR-ing the sign bit in is exact negation.
-    double o = from_bits(as_bits(q) | (long long)((unsigned long long)s << 63));
-    return z ? kSentinel : o;
+PCUB_HD double cv_pack(double q, uint32_t s) {
+    // q >= +0 (or NaN), so OR-ing the sign bit in is exact negation.
+    return from_bits(as_bits(q) | (long long)((unsigned long long)s << 63));
 }
 
-// max-normalise an un-normalised pair (p0, p1 >= 0) into compact form.
+// max-normalise an un-normalised pair (p0, p1 >= 0) into compact form;
+// (0, 0) gives 0/0 = NaN, the sentinel.
 PCUB_HD double norm_pack(double p0, double p1) {
     const bool sw = p1 > p0;
     const double num = sw ? p0 : p1;
     const double den = sw ? p1 : p0;
-    const bool z = den == 0.0;  // max == 0 => both zero
-    const double q = num / (z ? 1.0 : den);
-    return cv_pack(q, sw ? 1u : 0u, z);
+    return cv_pack(num / den, sw ? 1u : 0u);
 }
 
 // minus transform (BinaryMemorylessVectorDistribution.py:15-29) + normalise,
@@ -72,9 +75,8 @@ PCUB_HD double op_f(double va, double vb) {
     const double p1 = a.r + b.r;
     const bool sw = p1 > p0;
     const double num = sw ? p0 : p1;
-    const double den = sw ? p1 : p0;  // >= 1 unless an input is the sentinel
-    const double q = num / den;
-    return cv_pack(q, a.s ^ b.s ^ (sw ? 1u : 0u), a.z | b.z);
+    const double den = sw ? p1 : p0;  // in [1, 2], or NaN
+    return cv_pack(num / den, a.s ^ b.s ^ (sw ? 1u : 0u));
 }
 
 // plus transform (BinaryMemorylessVectorDistribution.py:31-47) + normalise.
@@ -83,20 +85,20 @@ PCUB_HD double op_f(double va, double vb) {
 // normalised ratio is min/max.
 PCUB_HD double op_g(double va, double vb, uint32_t u) {
     const CV a = cv_load(va), b = cv_load(vb);
-    bool z = a.z | b.z;
     double q;
     uint32_t s;
     if ((a.s ^ u) == b.s) {
         q = a.r * b.r;
         s = b.s;
     } else {
-        const double mx = a.r > b.r ? a.r : b.r;
-        const double mn = a.r > b.r ? b.r : a.r;
-        s = b.s ? (a.r > b.r ? 1u : 0u) : (b.r > a.r ? 1u : 0u);
-        z = z | (mx == 0.0);
-        q = mn / (mx == 0.0 ? 1.0 : mx);
+        // a NaN lands in mn (a) or mx (b) and the quotient is NaN; 0/0 is the (0, 0) output
+        const bool agt = a.r > b.r;
+        const double mx = agt ? a.r : b.r;
+        const double mn = agt ? b.r : a.r;
+        s = b.s ? (agt ? 1u : 0u) : (b.r > a.r ? 1u : 0u);
+        q = mn / mx;
     }
-    return cv_pack(q, s, z);
+    return cv_pack(q, s);
 }
 
 // raw (un-normalised) root rows: the root is never normalised by the reference.
@@ -123,7 +125,7 @@ PCUB_HD uint32_t leaf_f(double va, double vb) {
     const double p0 = 1.0 + m;
     const double p1 = a.r + b.r;
     const bool d = (a.s ^ b.s) ? (p0 > p1) : (p1 > p0);
-    return (d && !(a.z | b.z)) ? 1u : 0u;
+    return d ? 1u : 0u;
 }
 
 PCUB_HD uint32_t leaf_g(double va, double vb, uint32_t u) {
@@ -135,14 +137,14 @@ PCUB_HD uint32_t leaf_g(double va, double vb, uint32_t u) {
         // actual pair (x0, x1) = b.s ? (rb, ra) : (ra, rb)
         d = b.s ? (a.r > b.r) : (b.r > a.r);
     }
-    return (d && !(a.z | b.z)) ? 1u : 0u;
+    return d ? 1u : 0u;
 }
 
 // single leaf from a compact value: 1 <=> (r, 1) with r < 1.  (A tie (1,1) may
 // be stored as +1.0 or -1.0; both decide 0.)
 PCUB_HD uint32_t leaf_v(double v) {
     const CV a = cv_load(v);
-    return (a.s && !a.z && a.r < 1.0) ? 1u : 0u;
+    return (a.s && a.r < 1.0) ? 1u : 0u;
 }
 
 PCUB_HD uint32_t bitrev(uint32_t x, int nbits) {

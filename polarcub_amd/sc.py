@@ -112,6 +112,12 @@ def set_variant(v):
     _lib.check(_lib.lib().pcub_sc_set_variant(int(v)), "pcub_sc_set_variant")
 
 
+def set_max_blocks_per_cu(b):
+    """Cap resident decode workgroups per CU (0 = as many as fit); a tuning knob that
+    trades latency hiding against the cache footprint of the codewords in flight."""
+    _lib.check(_lib.lib().pcub_sc_set_max_blocks_per_cu(int(b)), "pcub_sc_set_max_blocks_per_cu")
+
+
 def variants():
     """[(S, G, W)] per decode kernel variant: register-subtree values per lane,
     lanes per codeword, minimum waves per SIMD."""

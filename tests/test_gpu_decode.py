@@ -21,7 +21,7 @@ def sc():
     return _sc
 
 
-@pytest.mark.parametrize("variant", range(13))
+@pytest.mark.parametrize("variant", range(15))
 @pytest.mark.parametrize("name", BIN_SETS)
 def test_decode_matches_reference(sc, name, variant):
     sc.set_variant(variant)
@@ -36,7 +36,7 @@ def test_decode_matches_reference(sc, name, variant):
     sc.set_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 3, 6, 7, 10])
+@pytest.mark.parametrize("variant", [0, 3, 6, 9, 11])
 @pytest.mark.parametrize("idx", range(24))
 def test_edge_cases(sc, idx, variant):
     sc.set_variant(variant)
@@ -48,7 +48,7 @@ def test_edge_cases(sc, idx, variant):
     assert np.array_equal(xhat.cpu().numpy(), c["xhat"])
 
 
-@pytest.mark.parametrize("variant", range(13))
+@pytest.mark.parametrize("variant", range(15))
 def test_ragged_batches_and_slot_reuse(sc, variant):
     """Batch sizes that are not tile multiples, and more tiles than resident slots."""
     from oracle import orc

@@ -30,11 +30,12 @@ constexpr int kBlock = 256;
 struct Variant {
     int S, G, W, L, T;
 };
-constexpr int kNumVariants = 15;
+constexpr int kNumVariants = 19;
 constexpr Variant kVar[kNumVariants] = {
     {16, 1, 2, 0, 0}, {8, 1, 4, 0, 0}, {32, 1, 1, 0, 0}, {16, 4, 2, 0, 0}, {8, 4, 4, 0, 0}, {16, 2, 2, 0, 0},
     {32, 2, 1, 0, 0}, {8, 8, 4, 0, 0}, {16, 2, 2, 0, 1}, {8, 8, 4, 0, 1}, {16, 4, 2, 0, 1}, {8, 4, 4, 1, 0},
-    {16, 2, 2, 0, 2}, {16, 4, 2, 0, 2}, {8, 4, 4, 0, 2},
+    {16, 2, 4, 0, 1}, {16, 4, 4, 0, 1}, {8, 4, 4, 0, 1}, {32, 4, 2, 0, 1}, {32, 2, 2, 0, 1},
+    {32, 4, 3, 0, 1}, {32, 2, 3, 0, 1},
 };
 
 size_t lds_bytes(int v) { return kVar[v].L ? (size_t)kVar[v].S * kBlock * sizeof(double2) : 0; }
@@ -53,6 +54,12 @@ __global__ __launch_bounds__(kBlock, W) void k_sc_bin(BinArgs A) {
         const bool valid = cw < A.B;
         decode_codeword<S, G, LDS, NT>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last);
     }
+}
+
+// rate-0 table: one byte per register subtree (first_frozen_depth)
+__global__ __launch_bounds__(kBlock) void k_ef_table(const uint32_t* fmask, int D, int SU, uint8_t* ef) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k < (1 << D)) ef[k] = (uint8_t)first_frozen_depth(fmask, k, D, SU);
 }
 
 template <int NN>
@@ -75,9 +82,13 @@ KernFn variant_kernel(int v) {
         case 9: return k_sc_bin<8, 8, 4, false, 1>;
         case 10: return k_sc_bin<16, 4, 2, false, 1>;
         case 11: return k_sc_bin<8, 4, 4, true, 0>;
-        case 12: return k_sc_bin<16, 2, 2, false, 2>;
-        case 13: return k_sc_bin<16, 4, 2, false, 2>;
-        case 14: return k_sc_bin<8, 4, 4, false, 2>;
+        case 12: return k_sc_bin<16, 2, 4, false, 1>;
+        case 13: return k_sc_bin<16, 4, 4, false, 1>;
+        case 14: return k_sc_bin<8, 4, 4, false, 1>;
+        case 15: return k_sc_bin<32, 4, 2, false, 1>;
+        case 16: return k_sc_bin<32, 2, 2, false, 1>;
+        case 17: return k_sc_bin<32, 4, 3, false, 1>;
+        case 18: return k_sc_bin<32, 2, 3, false, 1>;
         default: return k_sc_bin<16, 1, 2, false, 0>;
     }
 }
@@ -120,6 +131,16 @@ DevInfo dev_info() {
     cache = d;
     return d;
 }
+
+// subtree depth D = log2(Nv / S) and the rate-0 table's bytes (256-aligned)
+int tree_depth(int n, int v) {
+    int g = 0;
+    while ((1 << g) < kVar[v].G) ++g;
+    int s = 0;
+    while ((1 << s) < kVar[v].S) ++s;
+    return n - g - s;
+}
+size_t ef_bytes(int n, int v) { return (((size_t)1 << tree_depth(n, v)) + 255) & ~(size_t)255; }
 
 // per-slot bytes: virtual levels 1..D-1 (Nv/2 - S pairs) + Nv local encoding bits
 size_t slot_bytes(int n, int v) {
@@ -177,7 +198,7 @@ extern "C" size_t pcub_sc_decode_bin_workspace(int64_t B, int32_t log2N) {
     if (log2N < 6) return 0;
     const int v = pick_variant(log2N);
     const long long g = grid_for(B, v);
-    return (size_t)g * kBlock * slot_bytes(log2N, v);
+    return ef_bytes(log2N, v) + (size_t)g * kBlock * slot_bytes(log2N, v);
 }
 
 extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
@@ -199,6 +220,7 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
     A.scratch = nullptr;
     A.ybits = nullptr;
     A.nslots = 0;
+    A.ef = nullptr;
     if (log2N <= 5) {
         const dim3 grid((unsigned)((B + kBlock - 1) / kBlock));
         switch (log2N) {
@@ -216,13 +238,20 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
     if (g <= 0) return (int)hipErrorNoDevice;
     const size_t per_block = (size_t)kBlock * slot_bytes(log2N, v);
     if (!workspace) return PCUB_EINVAL;
-    if ((size_t)g * per_block > workspace_bytes) g = (long long)(workspace_bytes / per_block);
-    if (g <= 0) return PCUB_EINVAL;
+    const size_t efb = ef_bytes(log2N, v);
+    if (workspace_bytes < efb + per_block) return PCUB_EINVAL;
+    if ((size_t)g * per_block > workspace_bytes - efb) g = (long long)((workspace_bytes - efb) / per_block);
     const long long nslots = g * kBlock;
     const size_t Nv = ((size_t)1 << log2N) / kVar[v].G;
+    const int D = tree_depth(log2N, v);
+    uint8_t* ef = (uint8_t*)workspace;
+    char* slots = (char*)workspace + efb;
+    hipLaunchKernelGGL(k_ef_table, dim3((unsigned)(((1 << D) + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, frozen_mask,
+                       D, kVar[v].S * kVar[v].G, ef);
+    A.ef = ef;
     A.nslots = nslots;
-    A.scratch = (double2*)workspace;
-    A.ybits = (uint32_t*)((char*)workspace + (size_t)nslots * (Nv / 2 - kVar[v].S) * sizeof(double2));
+    A.scratch = (double2*)slots;
+    A.ybits = (uint32_t*)(slots + (size_t)nslots * (Nv / 2 - kVar[v].S) * sizeof(double2));
     hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), launch_lds(v), st, A);
     return (int)hipGetLastError();
 }

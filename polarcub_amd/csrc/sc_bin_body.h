@@ -44,7 +44,33 @@ struct BinArgs {
     double2* scratch;          // [(N_v/2 - S) pairs][nslots]
     uint32_t* ybits;           // [N_v/32][nslots]
     long long nslots;
+    const uint8_t* ef;         // [2^D] first rate-0 depth of each subtree's chain (first_frozen_depth)
 };
+
+// Rate-0 table.  Register subtree k (real u range [k*SU, (k+1)*SU)) is reached
+// by a chain that starts at depth d0(k) = 1 (k = 0) or D - ctz(k).  Returns the
+// smallest depth e in [d0, D] whose node on that chain has every u frozen, or
+// D + 1.  Such a node is never evaluated: nothing outside it reads it, and the
+// reference's decisions inside it are the frozen values.
+PCUB_HD bool range_frozen(const uint32_t* fmask, long long a, long long len) {
+    if (len < 32) {
+        const uint32_t m = ((1u << len) - 1u) << (a & 31);
+        return (fmask[a >> 5] & m) == m;
+    }
+    for (long long w = a >> 5; w < (a + len) >> 5; ++w)
+        if (fmask[w] != 0xffffffffu) return false;
+    return true;
+}
+
+PCUB_HD int first_frozen_depth(const uint32_t* fmask, int k, int D, int SU) {
+    const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
+    for (int e = d0; e <= D; ++e) {
+        const long long sub = 1LL << (D - e);  // register subtrees under a depth-e node
+        const long long first = ((long long)k >> (D - e)) << (D - e);
+        if (range_frozen(fmask, first * SU, sub * SU)) return e;
+    }
+    return D + 1;
+}
 
 #if defined(__HIP_DEVICE_COMPILE__)
 PCUB_HD double xor_shfl(double v, int mask) { return __shfl_xor(v, mask); }
@@ -67,8 +93,24 @@ struct XSub {
             ub |= ((uint64_t)u0 << UBASE) | ((uint64_t)u1 << (UBASE + 1));
             return lo ? (u0 ^ u1) : u1;
         } else {
-            const uint32_t ym = XSub<M / 2, UBASE>::run(op_f(a, b), ub, fm, fv, lane);
-            const uint32_t yp = XSub<M / 2, UBASE + M / 2>::run(op_g(a, b, ym), ub, fm, fv, lane);
+            // a frozen child (wave-uniform test) is not evaluated: its decisions are
+            // the frozen values and its encoding their polar transform
+            constexpr int H = M / 2;
+            constexpr uint64_t HM = (1ull << H) - 1ull;
+            const int pos = lane & (H - 1);
+            uint32_t ym, yp;
+            if (all_frozen<H>(fm, UBASE)) {
+                ym = frozen_local<1, H>(fv >> UBASE, pos) & 1u;
+                ub |= fv & (HM << UBASE);
+            } else {
+                ym = XSub<H, UBASE>::run(op_f(a, b), ub, fm, fv, lane);
+            }
+            if (all_frozen<H>(fm, UBASE + H)) {
+                yp = frozen_local<1, H>(fv >> (UBASE + H), pos) & 1u;
+                ub |= fv & (HM << (UBASE + H));
+            } else {
+                yp = XSub<H, UBASE + H>::run(op_g(a, b, ym), ub, fm, fv, lane);
+            }
             return lo ? (ym ^ yp) : yp;
         }
     }
@@ -89,14 +131,33 @@ struct SubV {
             ub |= ((uint64_t)u0 << BASE_V) | ((uint64_t)u1 << (BASE_V + 1));
             return (u0 ^ u1) | (u1 << 1);
         } else {
-            double c[L / 2];
+            // Rate-0 children (all u frozen; the test is wave-uniform) are skipped:
+            // the reference's decisions there are the frozen values whatever the
+            // probabilities, so only their re-encoding is needed.
+            constexpr int H = L / 2;
+            constexpr int HR = H * G;  // real leaves per child
+            constexpr uint64_t HM = (HR == 64) ? ~0ull : ((1ull << HR) - 1ull);
+            constexpr uint32_t LMASK = (H == 32) ? 0xffffffffu : ((1u << H) - 1u);
+            const int j = lane & (G - 1);
+            double c[H];
+            uint32_t ym, yp;
+            if (all_frozen<HR>(fm, BASE_V * G)) {
+                ym = frozen_local<H, G>(fv >> (BASE_V * G), j) & LMASK;
+                ub |= fv & (HM << (BASE_V * G));
+            } else {
 #pragma unroll
-            for (int t = 0; t < L / 2; ++t) c[t] = op_f(v[t], v[t + L / 2]);
-            const uint32_t ym = SubV<L / 2, BASE_V, G>::run(c, ub, fm, fv, lane);
+                for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
+                ym = SubV<H, BASE_V, G>::run(c, ub, fm, fv, lane);
+            }
+            if (all_frozen<HR>(fm, (BASE_V + H) * G)) {
+                yp = frozen_local<H, G>(fv >> ((BASE_V + H) * G), j) & LMASK;
+                ub |= fv & (HM << ((BASE_V + H) * G));
+            } else {
 #pragma unroll
-            for (int t = 0; t < L / 2; ++t) c[t] = op_g(v[t], v[t + L / 2], (ym >> t) & 1u);
-            const uint32_t yp = SubV<L / 2, BASE_V + L / 2, G>::run(c, ub, fm, fv, lane);
-            return (ym ^ yp) | (yp << (L / 2));
+                for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
+                yp = SubV<H, BASE_V + H, G>::run(c, ub, fm, fv, lane);
+            }
+            return (ym ^ yp) | (yp << H);
         }
     }
 };
@@ -342,6 +403,61 @@ PCUB_HD void dispatch_final(const Chain& c, Lvl l1, double* v, bool fg, bool roo
 // G lanes (`lane` = wave lane id, for the exchanges) in scratch slot `slot`.
 // S = virtual register subtree (values per lane) in {8, 16, 32}; requires
 // N >= 2*S*G and N >= 32*G.  `store` is false for padding codewords.
+// A register subtree's u decisions and frozen bits as NW 64-bit windows (a
+// subtree of more than 64 real positions is split at its top node, each half
+// into its own window).
+template <int S, int G>
+struct SubWin {
+    static constexpr int SU = S * G;
+    static constexpr int NW = SU > 64 ? 2 : 1;
+    static constexpr int SUW = SU > 64 ? 64 : SU;  // bits per window
+    static constexpr uint64_t WMASK = (SUW == 64) ? ~0ull : ((1ull << SUW) - 1ull);
+    static_assert(SU <= 128, "at most two windows");
+
+    // decisions of the subtree from its S level-D values
+    static PCUB_HD uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm, const uint64_t* fv, int lane) {
+        if constexpr (NW == 1) {
+            return SubV<S, 0, G>::run(v, ub[0], fm[0], fv[0], lane);
+        } else {
+            constexpr int H = S / 2;
+            const int j = lane & (G - 1);
+            double c[H];
+            uint32_t ym, yp;
+            if (all_frozen<64>(fm[0], 0)) {
+                ym = frozen_local<H, G>(fv[0], j);
+                ub[0] = fv[0];
+            } else {
+#pragma unroll
+                for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
+                ym = SubV<H, 0, G>::run(c, ub[0], fm[0], fv[0], lane);
+            }
+            if (all_frozen<64>(fm[1], 0)) {
+                yp = frozen_local<H, G>(fv[1], j);
+                ub[1] = fv[1];
+            } else {
+#pragma unroll
+                for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
+                yp = SubV<H, 0, G>::run(c, ub[1], fm[1], fv[1], lane);
+            }
+            return (ym ^ yp) | (yp << H);
+        }
+    }
+
+    // a rate-0 subtree: decisions = frozen values, encoding = their polar transform
+    static PCUB_HD uint32_t frozen(uint64_t* ub, const uint64_t* fv, int j) {
+        if constexpr (NW == 1) {
+            ub[0] = fv[0] & WMASK;
+            return frozen_local<S, G>(fv[0], j);
+        } else {
+            constexpr int H = S / 2;
+            ub[0] = fv[0];
+            ub[1] = fv[1];
+            const uint32_t ym = frozen_local<H, G>(fv[0], j), yp = frozen_local<H, G>(fv[1], j);
+            return (ym ^ yp) | (yp << H);
+        }
+    }
+};
+
 // NT: 0 = cached loads/stores, 1 = non-temporal input rows, 2 = also the upper stage levels
 template <int S, int G, bool LDS = false, int NT = 0>
 PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
@@ -351,9 +467,9 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     constexpr int s = (S == 8) ? 3 : (S == 16) ? 4 : 5;
     constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : (G == 4) ? 2 : 3;
     constexpr uint32_t SMASK = (S == 32) ? 0xffffffffu : ((1u << S) - 1u);
-    constexpr int SU = S * G;  // real u positions per register subtree (<= 64)
-    static_assert(SU <= 64, "u decisions of one subtree must fit 64 bits");
-    constexpr uint64_t SUMASK = (SU == 64) ? ~0ull : ((1ull << SU) - 1ull);
+    constexpr int SU = S * G;  // real u positions per register subtree (<= 128)
+    using W = SubWin<S, G>;
+    constexpr int NW = W::NW;
     constexpr int RR = NT >= 1 ? 2 : 1;
     constexpr bool NS = NT >= 2;
     const int n = A.n;
@@ -393,16 +509,51 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         // level is read from memory: every level written inside a chain is
         // consumed from registers by the next transform.
         const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
+        const int e0 = A.ef[k];  // first rate-0 depth on this chain (D + 1: none)
         int a = d0 - 1;
         bool fg = (k != 0);
-        int T = D - a;
-        const int Ffin = T >= 2 ? 2 : 1;
         Chain c;
         c.in = in;
         c.B = B;
         c.nv = nv;
         c.Y = Y;
         c.ns = ns;
+        // frozen bits of real u range [k*SU, (k+1)*SU), in NW windows
+        uint64_t fm[NW], fv[NW], ub[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const int us = k * SU + 64 * w;
+            const int uw = us >> 5, ush = us & 31;
+            if constexpr (W::SUW == 64) {
+                fm[w] = (uint64_t)A.fmask[uw] | ((uint64_t)A.fmask[uw + 1] << 32);
+                fv[w] = (uint64_t)A.fval[uw] | ((uint64_t)A.fval[uw + 1] << 32);
+            } else {
+                fm[w] = (uint64_t)((A.fmask[uw] >> ush) & (uint32_t)W::WMASK);
+                fv[w] = (uint64_t)((A.fval[uw] >> ush) & (uint32_t)W::WMASK);
+            }
+            ub[w] = 0;
+        }
+        uint32_t y;
+        if (e0 <= D - 1) {
+            // the chain enters a rate-0 node above the register level: evaluate
+            // (and store, for the plus children to come) only depths d0 .. e0-1
+            int T = e0 - 1 - a;
+            while (T > 0) {
+                const int F = T >= 3 ? 3 : T;
+                c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
+                c.ystart = (k >> (D - a)) << (nv - a);
+                const int La = Nv >> a;
+                if (F == 3) dispatch_pass<3, G, RR, NS>(c, La, lm, a, fg, a == 0);
+                else if (F == 2) dispatch_pass<2, G, RR, NS>(c, La, lm, a, fg, a == 0);
+                else dispatch_pass<1, G, RR, NS>(c, La, lm, a, fg, a == 0);
+                a += F;
+                T -= F;
+                fg = false;
+            }
+            y = W::frozen(ub, fv, j) & SMASK;
+        } else {
+        int T = D - a;
+        const int Ffin = T >= 2 ? 2 : 1;
         while (T > Ffin) {
             const int F = (T - Ffin) >= 3 ? 3 : (T - Ffin);
             c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
@@ -426,44 +577,45 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         } else {
             dispatch_final<S, 1, G, RR, NS, LDS>(c, lastlv, v, fg, true);
         }
-        // frozen bits of real u range [k*SU, (k+1)*SU)
-        const int ustart = k * SU;
-        const int uw = ustart >> 5, ush = ustart & 31;
-        uint64_t fm, fv;
-        if constexpr (SU == 64) {
-            fm = (uint64_t)A.fmask[uw] | ((uint64_t)A.fmask[uw + 1] << 32);
-            fv = (uint64_t)A.fval[uw] | ((uint64_t)A.fval[uw + 1] << 32);
+        if (e0 == D) {  // the register subtree itself is rate-0 (its level-D values go unused)
+            y = W::frozen(ub, fv, j) & SMASK;
         } else {
-            fm = (uint64_t)((A.fmask[uw] >> ush) & (uint32_t)SUMASK);
-            fv = (uint64_t)((A.fval[uw] >> ush) & (uint32_t)SUMASK);
+            y = W::run(v, ub, fm, fv, lane) & SMASK;
         }
-        uint64_t ub = 0;
-        const uint32_t y = SubV<S, 0, G>::run(v, ub, fm, fv, lane) & SMASK;
+        }
         // local encoding bits of virtual subtree k
         const int lstart = k * S;
         uint32_t* yw = Y + (long long)(lstart >> 5) * ns;
         if (S == 32) stu(yw, y);
         else stu(yw, ((lstart & 31) == 0 ? 0u : (ldu(yw) & ((1u << (lstart & 31)) - 1u))) | (y << (lstart & 31)));
         if (A.uout && store && j == 0) {
-            uint32_t* uo = A.uout + (long long)uw * B + cw;
-            if constexpr (SU == 64) {
-                uo[0] = (uint32_t)ub;
-                uo[B] = (uint32_t)(ub >> 32);
-            } else if constexpr (SU == 32) {
-                *uo = (uint32_t)ub;
-            } else {
-                *uo = (ush == 0 ? 0u : (*uo & ((1u << ush) - 1u))) | ((uint32_t)ub << ush);
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const int us = k * SU + 64 * w;
+                const int ush = us & 31;
+                uint32_t* uo = A.uout + (long long)(us >> 5) * B + cw;
+                if constexpr (W::SUW == 64) {
+                    uo[0] = (uint32_t)ub[w];
+                    uo[B] = (uint32_t)(ub[w] >> 32);
+                } else if constexpr (W::SUW == 32) {
+                    *uo = (uint32_t)ub[w];
+                } else {
+                    *uo = (ush == 0 ? 0u : (*uo & ((1u << ush) - 1u))) | ((uint32_t)ub[w] << ush);
+                }
             }
         }
         // information bits of this subtree, in u order (identical in all G lanes)
-        for (uint64_t im = ~fm & SUMASK; im != 0ull; im &= im - 1ull) {
-            const int q = __builtin_ctzll(im);
-            acc |= ((ub >> q) & 1ull) << nacc;
-            if (++nacc == 32) {
-                if (store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
-                acc = 0;
-                nacc = 0;
-                ++infow;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            for (uint64_t im = ~fm[w] & W::WMASK; im != 0ull; im &= im - 1ull) {
+                const int q = __builtin_ctzll(im);
+                acc |= ((ub[w] >> q) & 1ull) << nacc;
+                if (++nacc == 32) {
+                    if (store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
+                    acc = 0;
+                    nacc = 0;
+                    ++infow;
+                }
             }
         }
         // combine completed plus children upward: parent = [left ^ right | right]

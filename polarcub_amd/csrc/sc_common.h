@@ -147,6 +147,61 @@ PCUB_HD uint32_t leaf_v(double v) {
     return (a.s && a.r < 1.0) ? 1u : 0u;
 }
 
+// Re-encoding of known bits (frozen subtrees).  The half-split encoding of a
+// node, y = [y_minus ^ y_plus | y_plus], is the polar transform in natural
+// order: y_i = XOR of u_j over all j whose bits include i's.  Up to 64 bits.
+PCUB_HD uint64_t polar_bits(uint64_t x) {
+    x ^= (x >> 1) & 0x5555555555555555ull;
+    x ^= (x >> 2) & 0x3333333333333333ull;
+    x ^= (x >> 4) & 0x0F0F0F0F0F0F0F0Full;
+    x ^= (x >> 8) & 0x00FF00FF00FF00FFull;
+    x ^= (x >> 16) & 0x0000FFFF0000FFFFull;
+    x ^= (x >> 32) & 0x00000000FFFFFFFFull;
+    return x;
+}
+
+// Bits 0, G, 2G, .. of x, packed (the positions one lane of G owns).
+template <int G>
+PCUB_HD uint64_t gather_stride(uint64_t x) {
+    if constexpr (G == 1) {
+        return x;
+    } else if constexpr (G == 2) {
+        x &= 0x5555555555555555ull;
+        x = (x | (x >> 1)) & 0x3333333333333333ull;
+        x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+        x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+        x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+        return (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+    } else if constexpr (G == 4) {
+        x &= 0x1111111111111111ull;
+        x = (x | (x >> 3)) & 0x0303030303030303ull;
+        x = (x | (x >> 6)) & 0x000F000F000F000Full;
+        x = (x | (x >> 12)) & 0x000000FF000000FFull;
+        return (x | (x >> 24)) & 0x000000000000FFFFull;
+    } else {
+        static_assert(G == 8, "lanes per codeword");
+        x &= 0x0101010101010101ull;
+        x = (x | (x >> 7)) & 0x0003000300030003ull;
+        x = (x | (x >> 14)) & 0x0000000F0000000Full;
+        return (x | (x >> 28)) & 0x00000000000000FFull;
+    }
+}
+
+// Local encoding bits of a frozen node of LV values per lane spread over G
+// lanes (real length LV*G <= 64, known bits fv at bit 0), for lane position j.
+template <int LV, int G>
+PCUB_HD uint32_t frozen_local(uint64_t fv, int j) {
+    constexpr int R = LV * G;
+    const uint64_t m = (R == 64) ? ~0ull : ((1ull << R) - 1ull);
+    return (uint32_t)gather_stride<G>(polar_bits(fv & m) >> j);
+}
+
+template <int R>
+PCUB_HD bool all_frozen(uint64_t fm, int base) {
+    constexpr uint64_t m = (R == 64) ? ~0ull : ((1ull << R) - 1ull);
+    return ((fm >> base) & m) == m;
+}
+
 PCUB_HD uint32_t bitrev(uint32_t x, int nbits) {
     return nbits == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - nbits));
 }

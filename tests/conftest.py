@@ -34,3 +34,28 @@ def edge_cases():
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+def blocky_frozen(N, rng):
+    """A frozen set with aligned all-frozen (rate-0) and all-information blocks of
+    every size from 1 to N/4 plus scattered singles, and random frozen values:
+    exercises every rate-0 skip of the decode schedule."""
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    w = N // 4
+    while w >= 1:
+        for _ in range(2):
+            s = int(rng.integers(0, N // w)) * w
+            frozen[s:s + w] = int(rng.integers(0, 2))
+        w //= 2
+    frozen[: N // 8] = 1  # a leading rate-0 block, as in real polar codes
+    frozen[-1] = 0
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    return frozen, fval
+
+
+def awgn_like(B, N, rng, zeros=0.02):
+    llr = rng.normal(2.0, 2.0, (B, N)) * np.where(rng.random((B, N)) < 0.5, 1, -1)
+    p1 = 1.0 / (1.0 + np.exp(llr))
+    xy = np.stack([1.0 - p1, p1], axis=-1) * 0.5
+    xy[rng.random((B, N)) < zeros] = 0.0
+    return xy

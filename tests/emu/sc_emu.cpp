@@ -22,6 +22,7 @@ extern "C" int emu_decode_bin(const double* xy, long long B, int n, const uint32
     A.info = info;
     A.xhat = xhat;
     A.uout = uout;
+    A.ef = nullptr;
     if (n <= 5) {
         for (long long b = 0; b < B; ++b) {
             switch (n) {
@@ -39,6 +40,10 @@ extern "C" int emu_decode_bin(const double* xy, long long B, int n, const uint32
     if (N < 2 * S) return -1;
     std::vector<double2> scr((size_t)(N / 2 - S) * nslots + 1);
     std::vector<uint32_t> yb((size_t)(N / 32) * nslots);
+    const int D = n - (S == 8 ? 3 : S == 16 ? 4 : 5);
+    std::vector<uint8_t> ef((size_t)1 << D);
+    for (int k = 0; k < (1 << D); ++k) ef[k] = (uint8_t)first_frozen_depth(fmask, k, D, S);
+    A.ef = ef.data();
     A.scratch = scr.data();
     A.ybits = yb.data();
     A.nslots = nslots;
@@ -48,4 +53,31 @@ extern "C" int emu_decode_bin(const double* xy, long long B, int n, const uint32
         else decode_codeword<32, 1>(A, b, 0, 0, b % nslots, true);
     }
     return 0;
+}
+
+// helper self-checks: polar_bits against the half-split recursion, gather_stride against a bit loop
+static uint64_t enc_rec(uint64_t u, int L) {
+    if (L == 1) return u & 1u;
+    const uint64_t m = (L / 2 == 64) ? ~0ull : ((1ull << (L / 2)) - 1ull);
+    const uint64_t ym = enc_rec(u & m, L / 2), yp = enc_rec(u >> (L / 2), L / 2);
+    return (ym ^ yp) | (yp << (L / 2));
+}
+template <int G>
+static int check_gather(uint64_t x) {
+    for (int j = 0; j < G; ++j) {
+        uint64_t r = 0;
+        for (int t = 0; j + G * t < 64; ++t) r |= ((x >> (j + G * t)) & 1ull) << t;
+        if (gather_stride<G>(x >> j) != r) return 1;
+    }
+    return 0;
+}
+extern "C" int emu_check_bits(uint64_t seed) {
+    int bad = 0;
+    uint64_t x = seed;
+    for (int it = 0; it < 2000; ++it) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        if (polar_bits(x) != enc_rec(x, 64)) ++bad;
+        bad += check_gather<1>(x) + check_gather<2>(x) + check_gather<4>(x) + check_gather<8>(x);
+    }
+    return bad;
 }

@@ -64,3 +64,26 @@ def test_schedule_edge_cases(idx):
     c = edge_cases()[idx]
     info, xhat, _ = run(c["xy"], c["frozen"], c["fval"], 8)
     assert np.array_equal(info, c["info"]) and np.array_equal(xhat, c["xhat"])
+
+
+def test_bit_helpers():
+    assert emu().emu_check_bits(ctypes.c_uint64(0x9E3779B97F4A7C15)) == 0
+
+
+@pytest.mark.parametrize("S", [8, 16, 32])
+@pytest.mark.parametrize("n", [6, 7, 8, 10])
+def test_schedule_rate0_blocks(n, S):
+    """Frozen sets full of aligned rate-0 blocks (skipped by the schedule) against the oracle."""
+    from oracle import orc
+    from tests.conftest import awgn_like, blocky_frozen
+    N = 1 << n
+    if N < 2 * S:
+        pytest.skip("code shorter than two register subtrees")
+    rng = np.random.default_rng(100 * n + S)
+    for _ in range(3):
+        frozen, fval = blocky_frozen(N, rng)
+        xy = awgn_like(40, N, rng)
+        info, xhat, u = run(xy, frozen, fval, S)
+        ri, rx = orc.decode_bin(xy, frozen, fval)
+        assert np.array_equal(info, ri) and np.array_equal(xhat, rx)
+        assert np.all(u[:, frozen == 1] == fval[frozen == 1])

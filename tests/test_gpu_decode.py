@@ -21,7 +21,7 @@ def sc():
     return _sc
 
 
-@pytest.mark.parametrize("variant", range(15))
+@pytest.mark.parametrize("variant", range(19))
 @pytest.mark.parametrize("name", BIN_SETS)
 def test_decode_matches_reference(sc, name, variant):
     sc.set_variant(variant)
@@ -48,7 +48,7 @@ def test_edge_cases(sc, idx, variant):
     assert np.array_equal(xhat.cpu().numpy(), c["xhat"])
 
 
-@pytest.mark.parametrize("variant", range(15))
+@pytest.mark.parametrize("variant", range(19))
 def test_ragged_batches_and_slot_reuse(sc, variant):
     """Batch sizes that are not tile multiples, and more tiles than resident slots."""
     from oracle import orc
@@ -65,6 +65,26 @@ def test_ragged_batches_and_slot_reuse(sc, variant):
         ri, rx = orc.decode_bin(xy[sub], frozen, fval)
         assert np.array_equal(info.cpu().numpy()[sub], ri), (N, B)
         assert np.array_equal(xhat.cpu().numpy()[sub], rx), (N, B)
+    sc.set_variant(0)
+
+
+@pytest.mark.parametrize("variant", range(19))
+def test_rate0_blocks(sc, variant):
+    """Frozen sets full of aligned rate-0 blocks (skipped by every variant's schedule,
+    at the stage levels and inside the register and cross-lane subtrees)."""
+    from oracle import orc
+    from tests.conftest import awgn_like, blocky_frozen
+    sc.set_variant(variant)
+    rng = np.random.default_rng(7 + variant)
+    for n, B in [(6, 70), (7, 300), (8, 513), (10, 1000), (11, 200), (12, 64)]:
+        N = 1 << n
+        frozen, fval = blocky_frozen(N, rng)
+        xy = awgn_like(B, N, rng)
+        code = sc.CodeSpec(N, frozen, fval)
+        info, xhat = sc.BinaryDecoder(code).decode(torch.from_numpy(xy).cuda())
+        ri, rx = orc.decode_bin(xy, frozen, fval)
+        assert np.array_equal(info.cpu().numpy(), ri), (n, B)
+        assert np.array_equal(xhat.cpu().numpy(), rx), (n, B)
     sc.set_variant(0)
 
 

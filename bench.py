@@ -54,6 +54,20 @@ def make_inputs(code, B, sigma2, seed, device, chunk=1 << 18):
     return xy, info
 
 
+def measured_traffic(variant, n, batch):
+    """Per-launch HBM bytes of this exact decode configuration from the committed
+    rocprofv3 PMC passes (profiles/<round>/bin_v<variant>_n<n>/summary.json, written by
+    scripts/collect_profiles.py; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "bin_v%d_n%d" % (variant, n), "summary.json")),
+                       reverse=True):
+        with open(path) as f:
+            s = json.load(f)
+        if s.get("batch") == batch and "traffic_bytes" in s:
+            return s["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(code, xy_native, seconds_target=12.0):
     """The C oracle (oracle/sc_oracle.c, -O2 -ffp-contract=off) on the host cores, on a
     bounded sample of the same synthetic codewords (rank 0 only)."""
@@ -97,7 +111,7 @@ def main():
     ap.add_argument("--rate", type=float, default=0.5)
     ap.add_argument("--ebn0", type=float, default=2.0)
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU")
-    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--variant", type=int, default=None, help="decode kernel variant (default: the library's)")
     ap.add_argument("--max-blocks", type=int, default=0, help="cap decode workgroups per CU (0 = occupancy)")
     ap.add_argument("--seed", type=int, default=20250204)
     ap.add_argument("--no-cpu", action="store_true")
@@ -119,6 +133,7 @@ def main():
     frozen = construction.bhattacharyya_frozen(n, K, sigma2)
     code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(frozen)[0].tolist()), 1, device=device)
     sc.set_variant(args.variant)
+    variant = sc.default_variant() if args.variant is None else args.variant
     sc.set_max_blocks_per_cu(args.max_blocks)
     dec = sc.BinaryDecoder(code)
     B = args.batch
@@ -170,6 +185,7 @@ def main():
         avg_kern_s = float(np.mean(kern_ms)) / 1e3
         b_alg = 16 * N + N // 8 + K // 8  # f64 pairs in + packed x_hat + packed info, per codeword
         achieved = b_alg * B / avg_kern_s / 1e9
+        traffic, traffic_src = measured_traffic(variant, n, B)
         rec = {
             "metric": "decoded codewords/sec at N=%d BI-AWGN, batch=%d per GPU; FER match vs reference" % (N, B),
             "value": value,
@@ -184,12 +200,12 @@ def main():
             "dtype": "f64",
             "data": "synthetic: uniform info bits, GPU polar encoder, BI-AWGN Eb/N0=%.1f dB pairs generated on device" % args.ebn0,
             "config": {"workload": "binary SC decode N=%d K=%d BI-AWGN %.1f dB (BASELINE configs[1])" % (N, K, args.ebn0),
-                       "N": N, "K": K, "batch_per_gpu": B, "ebn0_db": args.ebn0, "kernel_variant": args.variant, "max_blocks_per_cu": args.max_blocks,
+                       "N": N, "K": K, "batch_per_gpu": B, "ebn0_db": args.ebn0, "kernel_variant": variant, "max_blocks_per_cu": args.max_blocks,
                        "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world},
             "fer": float(counters[1].item()) / int(counters[0].item()),
             "frame_errors": int(counters[1].item()),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_sc_bin", "kernel_ms": float(np.mean(kern_ms)),
                          "bytes_alg_per_cw": b_alg},
         }

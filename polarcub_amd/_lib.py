@@ -33,6 +33,8 @@ def lib():
     L.pcub_abi_version.restype = ctypes.c_int
     L.pcub_abi_version.argtypes = []
     L.pcub_sc_set_variant.restype = ctypes.c_int
+    L.pcub_sc_default_variant.restype = ctypes.c_int
+    L.pcub_sc_default_variant.argtypes = []
     L.pcub_sc_set_variant.argtypes = [ctypes.c_int]
     L.pcub_sc_set_max_blocks_per_cu.restype = ctypes.c_int
     L.pcub_sc_set_max_blocks_per_cu.argtypes = [ctypes.c_int]

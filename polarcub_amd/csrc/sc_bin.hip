@@ -93,7 +93,9 @@ KernFn variant_kernel(int v) {
     }
 }
 
-int g_variant = 0;
+// {32, 4, 3, NT}: fastest at N=1024 on MI355X (profiles/r1/sweep_*.txt)
+constexpr int kDefaultVariant = 17;
+int g_variant = kDefaultVariant;
 int g_max_blocks = 0;  // workgroups per CU cap (0 = as many as fit)
 constexpr size_t kLdsPerCu = 160 * 1024;
 
@@ -160,12 +162,18 @@ long long grid_for(long long B, int v) {
 }
 
 // a variant needs at least one outer level (N >= 2*S*G) and whole-word x_hat
-// segments (N >= 32*G); otherwise fall back to the 8-leaf one-lane variant.
-int pick_variant(int n) {
-    int v = g_variant;
+// segments (N >= 32*G); otherwise fall back to the first variant of a
+// decreasing-subtree list that fits (v1 = {8, 1} fits every N >= 64).
+bool fits(int v, int n) {
     const long long N = 1LL << n;
-    if (N < 2LL * kVar[v].S * kVar[v].G || N < 32LL * kVar[v].G) v = 1;
-    return v;
+    return N >= 2LL * kVar[v].S * kVar[v].G && N >= 32LL * kVar[v].G;
+}
+int pick_variant(int n) {
+    if (fits(g_variant, n)) return g_variant;
+    constexpr int kFallback[] = {17, 13, 14, 10, 0, 1};
+    for (int v : kFallback)
+        if (fits(v, n)) return v;
+    return 1;
 }
 
 }  // namespace
@@ -187,6 +195,7 @@ extern "C" int pcub_sc_set_max_blocks_per_cu(int b) {
     return 0;
 }
 
+extern "C" int pcub_sc_default_variant(void) { return kDefaultVariant; }
 extern "C" int pcub_sc_set_variant(int v) {
     if (v < 0 || v >= kNumVariants) return PCUB_EINVAL;
     g_variant = v;

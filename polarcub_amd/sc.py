@@ -107,8 +107,15 @@ class CodeSpec:
         return max(1, (self.N + 31) // 32)
 
 
-def set_variant(v):
-    """Select the decode kernel variant (see variants())."""
+def default_variant():
+    """The decode kernel variant the library picks unless told otherwise."""
+    return int(_lib.lib().pcub_sc_default_variant())
+
+
+def set_variant(v=None):
+    """Select the decode kernel variant (see variants()); None restores the default."""
+    if v is None:
+        v = default_variant()
     _lib.check(_lib.lib().pcub_sc_set_variant(int(v)), "pcub_sc_set_variant")
 
 

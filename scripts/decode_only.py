@@ -14,7 +14,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=10)
 ap.add_argument("--batch", type=int, default=1 << 20)
 ap.add_argument("--reps", type=int, default=3)
-ap.add_argument("--variant", type=int, default=0)
+ap.add_argument("--variant", type=int, default=None)
 a = ap.parse_args()
 N = 1 << a.n
 K = N // 2

@@ -33,7 +33,7 @@ def test_decode_matches_reference(sc, name, variant):
     torch.cuda.synchronize()
     assert np.array_equal(info.cpu().numpy(), g["info"])
     assert np.array_equal(xhat.cpu().numpy(), g["xhat"])
-    sc.set_variant(0)
+    sc.set_variant()
 
 
 @pytest.mark.parametrize("variant", [0, 3, 6, 9, 11])
@@ -65,7 +65,7 @@ def test_ragged_batches_and_slot_reuse(sc, variant):
         ri, rx = orc.decode_bin(xy[sub], frozen, fval)
         assert np.array_equal(info.cpu().numpy()[sub], ri), (N, B)
         assert np.array_equal(xhat.cpu().numpy()[sub], rx), (N, B)
-    sc.set_variant(0)
+    sc.set_variant()
 
 
 @pytest.mark.parametrize("variant", range(19))
@@ -85,7 +85,7 @@ def test_rate0_blocks(sc, variant):
         ri, rx = orc.decode_bin(xy, frozen, fval)
         assert np.array_equal(info.cpu().numpy(), ri), (n, B)
         assert np.array_equal(xhat.cpu().numpy(), rx), (n, B)
-    sc.set_variant(0)
+    sc.set_variant()
 
 
 @pytest.mark.parametrize("n", [1, 3, 5, 8, 10])

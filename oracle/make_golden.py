@@ -418,6 +418,152 @@ def fx_harness(R, timing):
     save("harness_bsc_n64", dict(N=N, trials=T, global_seed=seed, p=0.11, line=line), frozen=g["frozen"])
 
 
+def deletion_closures(R, n, n0, pd, xi, ones, channel_seed):
+    """The main_deletion.py:17-59 closures, rebuilt from the reference modules (main_deletion.py
+    itself runs main() on import)."""
+    import Guardbands as GB
+    BMD, BT, CBT = R["BMD"], R["BT"], R["CBT"]
+    N = 1 << n
+
+    def make_x():
+        xd = BMD.BinaryMemorylessDistribution()
+        xd.probs.append([0.5, 0.5])
+        return xd.makeBinaryMemorylessVectorDistribution(N, None)
+
+    def make_codeword(enc):
+        return GB.addDeletionGuardBands(enc, n, n0, xi, ones)
+
+    rng = random.Random()
+    rng.seed(channel_seed)
+
+    def channel(cw):
+        return BT.deletionChannelSimulation(cw, pd, seed=None, randomNumberGenerator=rng)
+
+    def make_xy(received, verbosity=0):
+        return CBT.buildCollectionOfBinaryTrellises_uniformInput_deletion(received, pd, xi, n, n0, ones, verbosity)
+
+    return make_x, make_codeword, channel, make_xy
+
+
+def ref_deletion_trials(R, n, n0, pd, xi, ones, frozen, crs, info_seed, channel_seed, T, rx_override=None):
+    """encodeDecodeSimulation (BinaryPolarEncoderDecoder.py:328-387) unrolled so that every
+    received word, transmitted/decoded information, x_hat and leaf marginal is recorded."""
+    BPED = R["BPED"]
+    N = 1 << n
+    make_x, make_codeword, channel, make_xy = deletion_closures(R, n, n0, pd, xi, ones, channel_seed)
+    xvd = make_x()
+    enc = BPED.BinaryPolarEncoderDecoder(N, frozen, crs)
+    irng = random.Random()
+    irng.seed(info_seed)
+    words, tx, info, xhat, leaf = [], [], [], [], []
+    t0 = time.perf_counter()
+    for t in range(T):
+        inf = [0 if irng.random() < 0.5 else 1 for _ in range(enc.k)]
+        cw = make_codeword(enc.encode(xvd, inf))
+        rx = channel(cw) if rx_override is None else list(rx_override[t])
+        with LeafRecorder(R) as lr:
+            xh, di = enc.decode(xvd, make_xy(rx))
+        assert len(lr.rec) == N
+        words.append(rx)
+        tx.append(inf)
+        info.append(list(di))
+        xhat.append(list(xh))
+        leaf.append(lr.rec)
+    dt = (time.perf_counter() - t0) / max(T, 1)
+    W = max([len(w) for w in words] + [1])
+    rx = np.zeros((T, W), np.uint8)
+    for t, w in enumerate(words):
+        rx[t, :len(w)] = w
+    lens = np.array([len(w) for w in words], np.int32)
+    mask, r, fval = frozen_arrays(enc, N)
+    return dict(rx=rx, rx_len=lens, tx_info=np.array(tx, np.uint8).reshape(T, enc.k),
+                info=np.array(info, np.uint8).reshape(T, enc.k), xhat=np.array(xhat, np.uint8),
+                leaf_m=np.array(leaf), frozen=mask, r=r, fval=fval, cw_len=len(cw)), dt
+
+
+def fx_deletion(R, timing):
+    """C5: main_deletion.py defaults (pd=0.1, xi=0.1, n0=n//3, ones=0, seeds cs=100 crs=200
+    gs=300 is=400) at n=8; frozen set from the reference's own genie
+    (genieEncodeDecodeSimulation, 100 trials, Pe bound 0.1, trustXYProbs=False)."""
+    import contextlib
+    import io
+    BPED = R["BPED"]
+    n, n0, pd, xi, ones = 8, 2, 0.1, 0.1, 0
+    N = 1 << n
+    make_x, make_codeword, channel, make_xy = deletion_closures(R, n, n0, pd, xi, ones, 100)
+    G = 100
+    buf = io.StringIO()
+    captured = {}
+    orig = BPED.frozenSetFromTVAndPe
+
+    def capture(TV, Pe, bound):
+        captured["score"] = [a + b for a, b in zip(TV, Pe)]
+        return orig(TV, Pe, bound)
+
+    BPED.frozenSetFromTVAndPe = capture
+    try:
+        with contextlib.redirect_stdout(buf):
+            frozen = BPED.genieEncodeDecodeSimulation(N, make_x, make_codeword, channel, make_xy, G, 0.1,
+                                                      genieSeed=300, trustXYProbs=False, filename=None)
+    finally:
+        BPED.frozenSetFromTVAndPe = orig
+    # The genie set at this trial count keeps very few information bits; the decode
+    # fixture uses the K = N/4 indices of smallest genie TV+Pe so that decisions matter.
+    score = captured["score"]
+    order = sorted(range(N), key=lambda i: (score[i], i))
+    frozen_dec = set(order[N // 4:])
+    T = 48
+    d, dt = ref_deletion_trials(R, n, n0, pd, xi, ones, frozen_dec, 200, 400, 100, T)
+    timing["deletion_n8_decode_s_per_cw"] = dt
+    errs = int(np.sum(np.any(d["info"] != d["tx_info"], axis=1)))
+    # the reference's own MC driver on the same closures: the printed line
+    make_x, make_codeword, channel, make_xy = deletion_closures(R, n, n0, pd, xi, ones, 100)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        BPED.encodeDecodeSimulation(N, make_x, make_codeword, channel, make_xy, 24, frozen,
+                                    commonRandomnessSeed=200, randomInformationSeed=400)
+    line = buf.getvalue().strip().splitlines()[-1]
+    print("  reference printed:", line, "| codeword length", d["cw_len"], "| K", N - len(frozen))
+    save("deletion_n8", dict(config="C5", n=n, n0=n0, pd=pd, xi=xi, ones=ones, crs=200, info_seed=400,
+                             channel_seed=100, genie_seed=300, genie_trials=G, trials=T, frame_errors=errs,
+                             mc_trials=24, line=line, cw_len=d.pop("cw_len"), genie_K=N - len(frozen),
+                             decode_frozen="K=N/4 smallest genie TV+Pe"),
+         genie_frozen=np.array([1 if i in frozen else 0 for i in range(N)], np.uint8),
+         genie_score=np.array(score), **d)
+
+
+def fx_deletion_edge(R, timing):
+    """Other (n, n0, pd) shapes, random frozen sets, and received words that break the
+    guard-band parse (segments longer than the trellis, empty, all-zero, raw random words)."""
+    rng = np.random.default_rng(42)
+    out = {}
+    cases = [(4, 1, 0.1, 0), (5, 2, 0.2, 0), (6, 2, 0.1, 0), (6, 3, 0.05, 0), (7, 2, 0.3, 0), (8, 2, 0.1, 0),
+             (9, 3, 0.1, 0), (5, 4, 0.1, 0), (4, 2, 0.1, 0), (6, 2, 0.1, 1), (5, 1, 0.15, 2)]
+    for ci, (n, n0, pd, ones) in enumerate(cases):
+        N = 1 << n
+        frozen = set(int(i) for i in np.nonzero(rng.random(N) < 0.5)[0])
+        T = 12 if n <= 8 else 6
+        crs = int(rng.integers(-1, 500))
+        d, _ = ref_deletion_trials(R, n, n0, pd, 0.1, ones, frozen, crs, int(rng.integers(1, 999)),
+                                   int(rng.integers(1, 999)), T)
+        # replace a few received words by adversarial ones (decoded by the reference again)
+        import Guardbands as GB
+        cwl = len(GB.addDeletionGuardBands([0] * N, n, n0, 0.1, ones))
+        adv = [list(w[:l]) for w, l in zip(d["rx"], d["rx_len"])]
+        adv[0] = []
+        adv[1] = [0] * (cwl // 2)
+        adv[2] = [int(b) for b in rng.integers(0, 2, cwl)]
+        adv[3] = [1] * (cwl - 3)
+        adv[4] = [int(b) for b in rng.integers(0, 2, max(1, cwl // 3))]
+        d, _ = ref_deletion_trials(R, n, n0, pd, 0.1, ones, frozen, crs, 1, 1, T, rx_override=adv)
+        d.pop("cw_len")
+        for k, v in d.items():
+            out["c%d_%s" % (ci, k)] = v
+        out["c%d_shape" % ci] = np.array([n, n0, ones], np.int32)
+        out["c%d_pd" % ci] = np.array([pd])
+    save("deletion_edge", dict(cases=len(cases), note="(n, n0, pd, ones) per case; words 0-4 adversarial"), **out)
+
+
 FIXTURES = {
     "bsc_n64": fx_bsc_n64,
     "awgn_n1024": lambda R, t: fx_awgn(R, t, 10, 64, 2.0, 20250204, "awgn_n1024", "C2"),
@@ -428,6 +574,8 @@ FIXTURES = {
     "encode_binary": fx_encode,
     "qsc_q4_n256": fx_qsc,
     "harness_bsc_n64": fx_harness,
+    "deletion_n8": fx_deletion,
+    "deletion_edge": fx_deletion_edge,
 }
 
 

@@ -89,6 +89,21 @@ int pcub_polar_encode_qary(const uint8_t* info, int64_t B, int32_t log2N, int32_
 int pcub_polar_encode_bin(const uint32_t* info_words, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
                           const uint32_t* frozen_val, int32_t K, uint32_t* x_words, void* stream);
 
+/* SC decode over the deletion channel (uniform input, no guard-band ones): replaces
+ * BinaryPolarEncoderDecoder.decode (BinaryPolarEncoderDecoder.py:71-99) over the
+ * CollectionOfBinaryTrellises that buildCollectionOfBinaryTrellises_uniformInput_deletion
+ * (VectorDistributions/CollectionOfBinaryTrellises.py:106-129, BinaryTrellis.py:309-438,
+ * Guardbands.py:47-93) builds from each received word.
+ *   rx          [B][stride] u8 received symbols (0/1), rx_len[b] <= stride of them valid
+ *   n, n0       code length 2^n, 2^n0 inputs per trellis; supported: 1 <= n0 <= 3,
+ *               1 <= n - n0 <= 6 (pcub_sc_deletion_supported)
+ *   pd          deletion probability the trellises are built with
+ *   frozen_mask / frozen_val / K / info_words / xhat_words as pcub_sc_decode_bin. */
+int pcub_sc_deletion_supported(int32_t n, int32_t n0);
+int pcub_sc_decode_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n, int32_t n0,
+                            double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K,
+                            uint32_t* info_words, uint32_t* xhat_words, void* stream);
+
 /* [B][nbits] u8 (0/1) -> ceil(nbits/32) x B words, and back. */
 int pcub_pack_bits(const uint8_t* bits, int64_t B, int32_t nbits, uint32_t* words, void* stream);
 int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits, uint8_t* bits, void* stream);

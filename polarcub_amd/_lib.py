@@ -62,6 +62,11 @@ def lib():
     L.pcub_unpack_bits.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p]
     L.pcub_transpose_pairs.restype = ctypes.c_int
     L.pcub_transpose_pairs.argtypes = [_c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p]
+    L.pcub_sc_deletion_supported.restype = ctypes.c_int
+    L.pcub_sc_deletion_supported.argtypes = [_i32, _i32]
+    L.pcub_sc_decode_deletion.restype = ctypes.c_int
+    L.pcub_sc_decode_deletion.argtypes = [_c_void_p, _c_void_p, _i64, _i32, _i32, _i32, ctypes.c_double, _c_void_p,
+                                          _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p]
     if L.pcub_abi_version() != 1:
         raise ImportError("libpolarcub_hip.so ABI mismatch; rebuild with python -m polarcub_amd.build --force")
     _lib = L
@@ -71,7 +76,8 @@ def lib():
 # every exported symbol declared in include/polarcub_sc.h
 EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_bin", "pcub_polar_encode_bin",
            "pcub_sc_decode_qary_workspace", "pcub_sc_decode_qary", "pcub_polar_encode_qary",
-           "pcub_pack_bits", "pcub_unpack_bits", "pcub_transpose_pairs"]
+           "pcub_pack_bits", "pcub_unpack_bits", "pcub_transpose_pairs", "pcub_sc_deletion_supported",
+           "pcub_sc_decode_deletion"]
 
 
 def check(rc, what):

@@ -13,12 +13,16 @@ reference, so harnesses written against polarcub run unchanged:
   polarTransformOfBits(xvec)                                          :494-516
   frozenSetFromTVAndPe(TVvec, Pevec, bound)                           :519-548
 
-Dispatch.  decode()/encode() of a *memoryless* binary distribution under a
-*uniform* a-priori distribution (every row p0 == p1: the a-priori tree is then
-(1,1) at every node) run on the GPU through the HIP C ABI -- bit-identical to
-the reference.  Any other plugin (trellises, user classes, non-uniform priors)
-goes through recursiveEncodeDecode, which drives the plugin's own methods
-exactly as the reference does.  Additions: decode_batch / encode_batch.
+Dispatch.  Under a *uniform* a-priori distribution (every row p0 == p1: the
+a-priori tree is then (1,1) at every node) decode() runs on the GPU through the
+HIP C ABI, bit-identical to the reference, for
+  * a memoryless binary xy distribution (pcub_sc_decode_bin), and
+  * a deletion-channel collection of trellises built from a received word by
+    buildCollectionOfBinaryTrellises_uniformInput_deletion, in the shapes the
+    deletion kernel covers (pcub_sc_decode_deletion).
+Any other plugin (other trellis shapes, user classes, non-uniform priors) goes
+through recursiveEncodeDecode, which drives the plugin's own methods exactly as
+the reference does.  Additions: decode_batch / encode_batch / decode_deletion_batch.
 """
 import random
 import sys
@@ -26,7 +30,7 @@ from enum import Enum
 
 import numpy as np
 
-from . import vectors
+from . import deletion, vectors
 
 
 class uIndexType(Enum):
@@ -44,6 +48,17 @@ def _is_uniform_prior(xvd):
         return False
     p = np.asarray(xvd.probs, dtype=np.float64)
     return p.ndim == 2 and p.shape[1] == 2 and bool(np.all(p[:, 0] == p[:, 1])) and bool(np.all(np.isfinite(p)))
+
+
+def _deletion_kernel_shape(xyvd):
+    """(pd, n, n0) when xyvd is a received-word trellis collection the deletion kernel decodes."""
+    if not deletion.is_deletion_collection(xyvd):
+        return None
+    word, pd, n, n0, ones = xyvd.deletion_source
+    if ones != 0:
+        return None
+    from . import sc
+    return (pd, n, n0) if sc.deletion_supported(n, n0) else None
 
 
 def _check_joint(p):
@@ -69,6 +84,7 @@ class BinaryPolarEncoderDecoder:
         self._device_code = None
         self._device_key = None
         self._decoder = None
+        self._del_decoders = {}
         self.initializeFrozenOrInformationAndRandomlyGeneratedNumbers()
 
     def initializeFrozenOrInformationAndRandomlyGeneratedNumbers(self):
@@ -97,6 +113,7 @@ class BinaryPolarEncoderDecoder:
             fval = np.where(0.5 >= self.randomlyGeneratedNumbers, 0, 1).astype(np.uint8)
             self._device_code = sc.CodeSpec(self.length, self._frozen_mask, fval)
             self._decoder = sc.BinaryDecoder(self._device_code)
+            self._del_decoders = {}
             self._device_key = key
         return self._device_code
 
@@ -112,6 +129,20 @@ class BinaryPolarEncoderDecoder:
             t = torch.from_numpy(_check_joint(xy)).to(code.device)
         assert t.dim() == 3 and t.shape[1] == self.length and t.shape[2] == 2
         info, xhat = self._decoder.decode(t)
+        return xhat.cpu().numpy().astype(np.int64), info.cpu().numpy().astype(np.int64)
+
+    def decode_deletion_batch(self, receivedWords, deletionProb, n0):
+        """Received words (0/1 sequences) of the deletion channel -> (encodedVectors int64[B, N],
+        information int64[B, k]); the same result as decode() on each word's
+        buildCollectionOfBinaryTrellises_uniformInput_deletion(word, deletionProb, xi, n, n0, 0)."""
+        from . import sc
+        code = self._code()
+        key = (int(n0), float(deletionProb))
+        dec = self._del_decoders.get(key)
+        if dec is None:
+            dec = self._del_decoders[key] = sc.DeletionDecoder(code, n0, deletionProb)
+        rx, ln = sc.pad_words(receivedWords, code.device)
+        info, xhat = dec.decode(rx, ln)
         return xhat.cpu().numpy().astype(np.int64), info.cpu().numpy().astype(np.int64)
 
     def encode_batch(self, information):
@@ -140,6 +171,10 @@ class BinaryPolarEncoderDecoder:
         if _is_memoryless_binary(xyVectorDistribution) and _is_uniform_prior(xVectorDistribution):
             xy = _check_joint(xyVectorDistribution.probs)
             enc, info = self.decode_batch(xy[None, :, :])
+            return (enc[0], info[0])
+        shape = _deletion_kernel_shape(xyVectorDistribution)
+        if shape is not None and _is_uniform_prior(xVectorDistribution):
+            enc, info = self.decode_deletion_batch([xyVectorDistribution.deletion_source[0]], shape[0], shape[2])
             return (enc[0], info[0])
         information = np.empty(self.k, np.int64)
         information[:] = -1
@@ -268,23 +303,29 @@ def encodeDecodeSimulation(length, make_xVectorDistribution, make_codeword, simu
             encoded = encDec.encode_batch(infos)
         else:
             encoded = np.stack([encDec.encode(xvd, list(infos[t])) for t in range(T)])
-        batch_xy, pending = [], []
+        batch_xy, batch_del, pending = [], {}, []
         for t in range(T):
             codeword = make_codeword(encoded[t])
             received = simulateChannel(codeword)
             xyvd = make_xyVectrorDistribution(received)
+            shape = _deletion_kernel_shape(xyvd) if uniform else None
             if uniform and _is_memoryless_binary(xyvd):
+                pending.append((t, codeword, received, ("bin", len(batch_xy))))
                 batch_xy.append(_check_joint(xyvd.probs))
-                pending.append((t, codeword, received, None))
+            elif shape is not None:
+                words = batch_del.setdefault(shape, [])
+                pending.append((t, codeword, received, (shape, len(words))))
+                words.append(xyvd.deletion_source[0])
             else:
                 pending.append((t, codeword, received, encDec.decode(xvd, xyvd)[1]))
+        results = {}
         if batch_xy:
-            _, dec_info = encDec.decode_batch(np.stack(batch_xy))
-        j = 0
+            results["bin"] = encDec.decode_batch(np.stack(batch_xy))[1]
+        for shape, words in batch_del.items():
+            results[shape] = encDec.decode_deletion_batch(words, shape[0], shape[2])[1]
         for (t, codeword, received, info_t) in pending:
-            if info_t is None:
-                info_t = dec_info[j]
-                j += 1
+            if isinstance(info_t, tuple):
+                info_t = results[info_t[0]][info_t[1]]
             if np.any(info_t != infos[t]):
                 errors += 1
                 if verbosity > 0:

@@ -193,7 +193,11 @@ template <int LV, int G>
 PCUB_HD uint32_t frozen_local(uint64_t fv, int j) {
     constexpr int R = LV * G;
     const uint64_t m = (R == 64) ? ~0ull : ((1ull << R) - 1ull);
-    return (uint32_t)gather_stride<G>(polar_bits(fv & m) >> j);
+    if constexpr (LV == 1) {
+        return (uint32_t)((polar_bits(fv & m) >> j) & 1ull);  // one value per lane, any G <= 64
+    } else {
+        return (uint32_t)gather_stride<G>(polar_bits(fv & m) >> j);
+    }
 }
 
 template <int R>

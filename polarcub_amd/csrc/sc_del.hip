@@ -1,0 +1,244 @@
+// sc_del.hip -- SC decoding over the deletion channel (collection of binary
+// trellises), gfx950, + its C-ABI launcher.
+//
+// pcub_sc_decode_deletion replaces BinaryPolarEncoderDecoder.decode
+// (BinaryPolarEncoderDecoder.py:71-99, recursion :223-325) when the xy vector
+// distribution is the CollectionOfBinaryTrellises built by
+// buildCollectionOfBinaryTrellises_uniformInput_deletion
+// (VectorDistributions/CollectionOfBinaryTrellises.py:106-129) from a received
+// word, for a batch of received words.
+//
+// Geometry.  T = 2^(n-n0) trellises per codeword -> T lanes per codeword (one
+// trellis per lane), 256/T codewords per 256-thread workgroup.  Lane position p
+// (lane & (T-1)) owns trellis bitrev(p): the collapsed memoryless node of length
+// T is then held in half-split order, one value per lane, and its SC subtree is
+// XSub<T> from sc_bin_body.h (cross-lane butterflies with __shfl_xor, the same
+// compact-pair arithmetic as the memoryless kernel).  Everything above it -- the
+// n0 trellis levels -- is lane-local: the plus transform of trellis t needs only
+// t's slice of the minus child's re-encoded vector
+// (CollectionOfBinaryTrellises.py:58-66), and the re-encoding combine
+// (BinaryPolarEncoderDecoder.py:319-323) maps trellis t's slices onto itself.
+//
+// Each lane keeps one trellis per depth (the current SC path) in private memory;
+// the schedule is identical in every lane, only trip counts of the small edge
+// loops differ.  Received words are read straight from HBM (u8, row per
+// codeword, a few hundred bytes each, L1/L2-resident while a group works on them).
+#include <hip/hip_runtime.h>
+
+#include "polarcub_sc.h"
+#include "sc_bin_body.h"
+#include "trellis_body.h"
+
+using namespace pcub;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct DelArgs {
+    const uint8_t* rx;      // [B][stride] received symbols (0/1)
+    const int32_t* rx_len;  // [B]
+    long long B;
+    int stride;
+    int n;
+    double pd;
+    const uint32_t* fmask;
+    const uint32_t* fval;
+    uint32_t* info;         // [ceil(K/32)][B]
+    uint32_t* xhat;         // [ceil(N/32)][B] or null
+};
+
+// Per-lane decoding context: frozen windows, decisions, information accumulator.
+template <int T>
+struct DelCtx {
+    const DelArgs* A;
+    long long cw;
+    bool leader;  // group position 0 stores the information words
+    int lane;
+    int k;        // next memoryless subtree (u range [k*T, (k+1)*T))
+    uint32_t acc;
+    int nacc;
+    int infow;
+
+    PCUB_HD uint64_t window(const uint32_t* w) const {
+        const int us = k * T;
+        if constexpr (T == 64) {
+            return (uint64_t)w[us >> 5] | ((uint64_t)w[(us >> 5) + 1] << 32);
+        } else {
+            return (uint64_t)((w[us >> 5] >> (us & 31)) & (uint32_t)((1ull << T) - 1ull));
+        }
+    }
+
+    // SC over the collapsed memoryless node (one compact value per lane); returns
+    // this lane's bit of the node's re-encoded vector (natural position = its trellis).
+    __device__ uint32_t subtree(double v) {
+        const uint64_t fm = window(A->fmask), fv = window(A->fval);
+        uint64_t ub = 0;
+        uint32_t y;
+        constexpr uint64_t WM = (T == 64) ? ~0ull : ((1ull << T) - 1ull);
+        if (fm == WM) {  // rate-0 node: decisions are the frozen values
+            ub = fv;
+            y = frozen_local<1, T>(fv, lane & (T - 1));
+        } else {
+            y = XSub<T, 0>::run(v, ub, fm, fv, lane) & 1u;
+        }
+        for (uint64_t im = ~fm & WM; im != 0ull; im &= im - 1ull) {
+            acc |= (uint32_t)((ub >> __builtin_ctzll(im)) & 1ull) << nacc;
+            if (++nacc == 32) {
+                if (leader) A->info[(long long)infow * A->B + cw] = acc;
+                acc = 0;
+                nacc = 0;
+                ++infow;
+            }
+        }
+        ++k;
+        return y;
+    }
+};
+
+template <int L>
+struct DelCap {
+    static constexpr int V = L / 2 + 1;
+    static constexpr int E0 = 3 * V;      // base edge layer
+    static constexpr int E1 = 2 * V * V;  // transformed edge layer
+};
+
+// One SC node of the trellis levels: trellis `t` of length LEN (this lane's
+// slice of the collection).  Returns the node's re-encoded slice, natural order.
+template <int L, int T, int LEN>
+struct DelNode {
+    template <class PT>
+    __device__ static uint32_t run(const PT& t, DelCtx<T>& cx) {
+        using Cap = DelCap<L>;
+        if constexpr (LEN == 2) {
+            // children are length-1 trellises collapsed to memoryless rows
+            // (CollectionOfBinaryTrellises.py:68-82), then normalised by the decoder
+            Trel<1, Cap::V, Cap::E1> c;
+            double m0, m1;
+            trellis_transform<2>(t, c, nullptr);
+            trellis_marginal(c, m0, m1);
+            const uint32_t xm = cx.subtree(norm_pack(m0, m1));
+            trellis_transform<2>(t, c, &xm);
+            trellis_marginal(c, m0, m1);
+            const uint32_t xp = cx.subtree(norm_pack(m0, m1));
+            return (xm ^ xp) | (xp << 1);
+        } else {
+            constexpr int H = LEN / 2;
+            Trel<H, Cap::V, Cap::E1> c;
+            trellis_transform<LEN>(t, c, nullptr);
+            trellis_normalize<H>(c);
+            const uint32_t ym = DelNode<L, T, H>::run(c, cx);
+            trellis_transform<LEN>(t, c, &ym);
+            trellis_normalize<H>(c);
+            const uint32_t yp = DelNode<L, T, H>::run(c, cx);
+            uint32_t x = 0;  // x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h]
+#pragma unroll
+            for (int h = 0; h < H; ++h)
+                x |= ((((ym ^ yp) >> h) & 1u) << (2 * h)) | (((yp >> h) & 1u) << (2 * h + 1));
+            return x;
+        }
+    }
+};
+
+template <int N0, int TB>
+__global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
+    constexpr int L = 1 << N0;
+    constexpr int T = 1 << TB;
+    constexpr int CPB = kBlock / T;          // codewords per workgroup
+    constexpr int NB = T * L;                // code length N
+    constexpr int WPC = (NB + 31) / 32;      // x_hat words per codeword
+    using Cap = DelCap<L>;
+    __shared__ uint32_t xs[CPB * WPC];
+
+    const int lane = threadIdx.x & 63;
+    const int p = threadIdx.x & (T - 1);
+    const int g = threadIdx.x >> TB;
+    const long long cw = (long long)blockIdx.x * CPB + g;
+    const bool valid = cw < A.B;
+    const long long c = valid ? cw : A.B - 1;  // padding groups decode a duplicate, store nothing
+    for (int i = threadIdx.x; i < CPB * WPC; i += kBlock) xs[i] = 0;
+
+    const uint8_t* w = A.rx + c * (long long)A.stride;
+    int len = A.rx_len[c];
+    len = len < 0 ? 0 : (len > A.stride ? A.stride : len);
+    auto bit = [w](int i) { return (int)w[i]; };
+    const int t = (int)bitrev((uint32_t)p, TB);
+    int s, m;
+    segment_of(bit, len, TB, t, s, m);
+
+    Trel<L, Cap::V, Cap::E0> base;
+    trellis_build<L>(base, bit, s, m, A.pd);
+
+    DelCtx<T> cx;
+    cx.A = &A;
+    cx.cw = cw;
+    cx.leader = valid && p == 0;
+    cx.lane = lane;
+    cx.k = 0;
+    cx.acc = 0;
+    cx.nacc = 0;
+    cx.infow = 0;
+    const uint32_t x = DelNode<L, T, L>::run(base, cx);
+    if (cx.nacc && cx.leader) A.info[(long long)cx.infow * A.B + cw] = cx.acc;
+
+    // x_hat: trellis t's slice is natural positions [t*L, (t+1)*L)
+    __syncthreads();
+    const int pos = t * L;
+    atomicOr(&xs[g * WPC + (pos >> 5)], (x & ((1u << L) - 1u)) << (pos & 31));
+    __syncthreads();
+    if (A.xhat && valid)
+        for (int i = p; i < WPC; i += T) A.xhat[(long long)i * A.B + cw] = xs[g * WPC + i];
+}
+
+typedef void (*DelKern)(DelArgs);
+
+template <int N0>
+DelKern del_kernel_tb(int tb) {
+    switch (tb) {
+        case 1: return k_sc_del<N0, 1>;
+        case 2: return k_sc_del<N0, 2>;
+        case 3: return k_sc_del<N0, 3>;
+        case 4: return k_sc_del<N0, 4>;
+        case 5: return k_sc_del<N0, 5>;
+        case 6: return k_sc_del<N0, 6>;
+        default: return nullptr;
+    }
+}
+
+DelKern del_kernel(int n0, int tb) {
+    switch (n0) {
+        case 1: return del_kernel_tb<1>(tb);
+        case 2: return del_kernel_tb<2>(tb);
+        case 3: return del_kernel_tb<3>(tb);
+        default: return nullptr;
+    }
+}
+
+}  // namespace
+
+extern "C" int pcub_sc_deletion_supported(int32_t n, int32_t n0) { return del_kernel(n0, n - n0) != nullptr; }
+
+extern "C" int pcub_sc_decode_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n,
+                                       int32_t n0, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
+                                       int32_t K, uint32_t* info_words, uint32_t* xhat_words, void* stream) {
+    const DelKern kern = del_kernel(n0, n - n0);
+    if (!kern || B < 0 || stride < 0 || stride > 32767 || !frozen_mask || !frozen_val) return PCUB_EINVAL;
+    if (K < 0 || K > (1 << n) || (K > 0 && !info_words) || (B > 0 && (!rx || !rx_len))) return PCUB_EINVAL;
+    if (!(pd >= 0.0 && pd <= 1.0)) return PCUB_EINVAL;
+    if (B == 0) return 0;
+    DelArgs A;
+    A.rx = rx;
+    A.rx_len = rx_len;
+    A.B = B;
+    A.stride = stride;
+    A.n = n;
+    A.pd = pd;
+    A.fmask = frozen_mask;
+    A.fval = frozen_val;
+    A.info = info_words;
+    A.xhat = xhat_words;
+    const long long cpb = kBlock >> (n - n0);
+    const long long grid = (B + cpb - 1) / cpb;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, A);
+    return (int)hipGetLastError();
+}

@@ -1,0 +1,209 @@
+// trellis_body.h -- deletion-channel trellis stages of the SC decoder (host + device).
+//
+// Replaces, per (codeword, trellis) lane:
+//   Guardbands.removeDeletionGuardBands / trimZerosAtEdges    Guardbands.py:47-93
+//   BinaryTrellis.buildTrellis_uniformInput_deletion          VectorDistributions/BinaryTrellis.py:309-438
+//   BinaryTrellis.__miusPlusTransform                         VectorDistributions/BinaryTrellis.py:206-258
+//   BinaryTrellis.calcNormalizationVector / normalize         VectorDistributions/BinaryTrellis.py:280-306
+//   BinaryTrellis.calcMarginalizedProbabilities(normalize=False), as called by the
+//   collection collapse                                      VectorDistributions/CollectionOfBinaryTrellises.py:68-82
+// for a single-state, uniform-input trellis with no guard-band ones
+// (numberOfOnesToAddAtBothEndsOfGuardbands = 0, the main_deletion.py default).
+//
+// Order of floating-point sums.  The reference keeps vertices and edges in
+// insertion-ordered dicts and every sum (edge accumulation in a transform, the
+// per-layer normaliser, the marginal) runs in that order.  A vertex's out-edges
+// (in-edges) in dict order are exactly the edges leaving (entering) it in
+// CREATION order, so each edge layer is stored as an append-only array in
+// creation order, and each vertex layer as an append-only list of vpos values
+// in insertion order.  Iterating "vertices of layer i in order, then the edge
+// array filtered by from-vertex" is then the reference's iteration, and all
+// sums are formed in the same order (tests/test_trellis_* pin this bit-exactly).
+//
+// Capacities (ones = 0).  Base layer l of a trellis of length L with m received
+// symbols holds vpos in [max(0, l - (L - m)), min(l, m)]: at most L/2 + 1
+// vertices.  A transformed trellis's layer j is a subset of base layer j*2^d, so
+// every layer of every depth has at most V = L/2 + 1 vertices; a base edge layer
+// has at most 3V edges (one insertion, two deletions per vertex) and a
+// transformed one at most 2*V*V (one per (from, to, label)).
+#pragma once
+#include "sc_common.h"
+
+namespace pcub {
+
+// edge key: from vpos (15 bits) | to vpos (15 bits) | label
+PCUB_HD uint32_t ekey(int u, int v, int x) { return ((uint32_t)u << 16) | ((uint32_t)v << 1) | (uint32_t)x; }
+PCUB_HD int ek_from(uint32_t k) { return (int)(k >> 16); }
+PCUB_HD int ek_to(uint32_t k) { return (int)((k >> 1) & 0x7fffu); }
+PCUB_HD int ek_lbl(uint32_t k) { return (int)(k & 1u); }
+
+template <int LEN, int V, int E>
+struct Trel {
+    int8_t nv[LEN + 1];     // vertices per layer
+    int16_t vp[LEN + 1][V]; // vpos in insertion order
+    int8_t ne[LEN];         // edges per edge layer
+    uint32_t key[LEN][E];   // creation order
+    double p[LEN][E];
+
+    PCUB_HD void clear() {
+        for (int l = 0; l <= LEN; ++l) nv[l] = 0;
+        for (int l = 0; l < LEN; ++l) ne[l] = 0;
+    }
+    // __getVertexAndAddIfNeeded (BinaryTrellis.py:155-162)
+    PCUB_HD void vertex(int l, int vpos) {
+        const int c = nv[l];
+        for (int i = 0; i < c; ++i)
+            if (vp[l][i] == vpos) return;
+        vp[l][c] = (int16_t)vpos;
+        nv[l] = (int8_t)(c + 1);
+    }
+    // addToEdgeProb (BinaryTrellis.py:128-136): from-vertex, to-vertex, then the edge (+= p)
+    PCUB_HD void add(int l, int u, int v, int x, double prob) {
+        vertex(l, u);
+        vertex(l + 1, v);
+        const uint32_t k = ekey(u, v, x);
+        const int c = ne[l];
+        for (int i = 0; i < c; ++i)
+            if (key[l][i] == k) {
+                p[l][i] += prob;
+                return;
+            }
+        key[l][c] = k;
+        p[l][c] = 0.0 + prob;
+        ne[l] = (int8_t)(c + 1);
+    }
+};
+
+template <int L>
+struct TrelCap {
+    static constexpr int V = L / 2 + 1;
+};
+
+// The base trellis of one segment, word[s .. s+m) (buildTrellis_uniformInput_deletion,
+// ones = 0, trimmed edges).  `bit(i)` returns received symbol i of the codeword.
+template <int L, class T, class BitF>
+PCUB_HD void trellis_build(T& t, const BitF& bit, int s, int m, double pd) {
+    t.clear();
+    const int dcount = L - m;
+    t.vertex(0, 0);  // setVertexProb: start vertex, prob 1.0
+    t.vertex(L, m);  // end vertex, prob 1.0
+    const double p_ins = 0.5 * (1.0 - pd);
+    const double p_del = 0.5 * pd;
+    for (int l = 0; l < L; ++l) {
+        const int lo = l - dcount > 0 ? l - dcount : 0;
+        const int hi = l < m ? l : m;
+        for (int vp = lo; vp <= hi; ++vp) {
+            if (vp < m) t.add(l, vp, vp + 1, bit(s + vp), p_ins);
+            if (l + 1 - dcount <= vp) {
+                // label 0 then 1; a deletion of a 0 at either trimmed edge is certain
+                t.add(l, vp, vp, 0, (vp > 0 && vp < m) ? p_del : 0.5);
+                t.add(l, vp, vp, 1, p_del);
+            }
+        }
+    }
+}
+
+// __miusPlusTransform (BinaryTrellis.py:206-258).  dec = nullptr: minus; else bit j
+// of *dec is decisionVector[j] (plus).
+template <int LEN, class P, class C>
+PCUB_HD void trellis_transform(const P& pt, C& ct, const uint32_t* dec) {
+    constexpr int H = LEN / 2;
+    ct.clear();
+    for (int i = 0; i < pt.nv[0]; ++i) ct.vertex(0, pt.vp[0][i]);
+    for (int i = 0; i < pt.nv[LEN]; ++i) ct.vertex(H, pt.vp[LEN][i]);
+    for (int j = 0; j < H; ++j) {
+        const int mid = 2 * j + 1;
+        const int dj = dec ? (int)((*dec >> j) & 1u) : 0;
+        for (int wi = 0; wi < pt.nv[mid]; ++wi) {
+            const int w = pt.vp[mid][wi];
+            for (int a = 0; a < pt.ne[mid - 1]; ++a) {
+                const uint32_t ka = pt.key[mid - 1][a];
+                if (ek_to(ka) != w) continue;
+                for (int b = 0; b < pt.ne[mid]; ++b) {
+                    const uint32_t kb = pt.key[mid][b];
+                    if (ek_from(kb) != w) continue;
+                    const double prob = pt.p[mid - 1][a] * pt.p[mid][b];
+                    const int ml = ek_lbl(ka) ^ ek_lbl(kb);
+                    if (!dec) {
+                        ct.add(j, ek_from(ka), ek_to(kb), ml, prob);
+                    } else if (ml == dj) {
+                        ct.add(j, ek_from(ka), ek_to(kb), ek_lbl(kb), prob);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// calcNormalizationVector + normalize (BinaryTrellis.py:280-306), as the decoder
+// applies them to every freshly transformed child.
+template <int LEN, class T>
+PCUB_HD void trellis_normalize(T& t) {
+    for (int i = 0; i < LEN; ++i) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int vi = 0; vi < t.nv[i]; ++vi) {
+            const int v = t.vp[i][vi];
+            for (int e = 0; e < t.ne[i]; ++e) {
+                const uint32_t k = t.key[i][e];
+                if (ek_from(k) != v) continue;
+                if (ek_lbl(k)) s1 += t.p[i][e];
+                else s0 += t.p[i][e];
+            }
+        }
+        double d = s0 >= s1 ? s0 : s1;  // np.maximum of two non-negative finite sums
+        if (d == 0.0) d = 1.0;
+        for (int e = 0; e < t.ne[i]; ++e) t.p[i][e] /= d;
+    }
+}
+
+// calcMarginalizedProbabilities(normalize=False) of a length-1 trellis
+// (BinaryTrellis.py:260-278): vertexProb * edgeProb * toVertex.vertexProb / 1.0,
+// all vertex probabilities 1.0 when ones = 0, so each term is the edge probability.
+template <class T>
+PCUB_HD void trellis_marginal(const T& t, double& m0, double& m1) {
+    m0 = 0.0;
+    m1 = 0.0;
+    for (int vi = 0; vi < t.nv[0]; ++vi) {
+        const int v = t.vp[0][vi];
+        for (int e = 0; e < t.ne[0]; ++e) {
+            const uint32_t k = t.key[0][e];
+            if (ek_from(k) != v) continue;
+            if (ek_lbl(k)) m1 += t.p[0][e];
+            else m0 += t.p[0][e];
+        }
+    }
+}
+
+// trimZerosAtEdges on word[s .. e): the first and last 1 (Guardbands.py:66-93).
+template <class BitF>
+PCUB_HD void trim_range(const BitF& bit, int& s, int& e) {
+    int a = s;
+    while (a < e && bit(a) != 1) ++a;
+    if (a == e) {
+        s = e = a;
+        return;
+    }
+    int b = e - 1;
+    while (bit(b) != 1) --b;
+    s = a;
+    e = b + 1;
+}
+
+// removeDeletionGuardBands (Guardbands.py:47-63) for one trellis: trim, halve
+// (left = first len/2), descend toward trellis index t (levels = n - n0 halvings,
+// most significant bit of t first), trim again at the end.
+template <class BitF>
+PCUB_HD void segment_of(const BitF& bit, int len, int levels, int t, int& s, int& m) {
+    int a = 0, e = len;
+    trim_range(bit, a, e);
+    for (int k = levels - 1; k >= 0; --k) {
+        const int h = (e - a) / 2;
+        if ((t >> k) & 1) a += h;
+        else e = a + h;
+        trim_range(bit, a, e);
+    }
+    s = a;
+    m = e - a;
+}
+
+}  // namespace pcub

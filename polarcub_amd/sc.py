@@ -297,3 +297,55 @@ def encode_qary(code, info):
     rc = _lib.lib().pcub_polar_encode_qary(_p(inf), B, code.n, code.q, _p(code.frozen_dev), code.K, _p(x), _stream())
     _lib.check(rc, "pcub_polar_encode_qary")
     return x.t().contiguous()
+
+
+def deletion_supported(n, n0):
+    """True when pcub_sc_decode_deletion has a kernel for 2^n0-input trellises and 2^(n-n0) of them."""
+    return bool(_lib.lib().pcub_sc_deletion_supported(int(n), int(n0)))
+
+
+class DeletionDecoder:
+    """Batched SC decoder over the deletion channel (CollectionOfBinaryTrellises built from
+    each received word with buildCollectionOfBinaryTrellises_uniformInput_deletion, no
+    guard-band ones) for one CodeSpec."""
+
+    def __init__(self, code, n0, pd):
+        self.code = code
+        self.n0 = int(n0)
+        self.pd = float(pd)
+        if not deletion_supported(code.n, self.n0):
+            raise ValueError("no deletion kernel for n=%d, n0=%d" % (code.n, self.n0))
+
+    def decode_native(self, rx, rx_len, want_xhat=True):
+        """rx: [B, W] uint8 received symbols on device, rx_len: [B] int32.
+        Returns packed (info_words [ceil(K/32), B], xhat_words [ceil(N/32), B] | None)."""
+        c = self.code
+        if rx.dtype != torch.uint8 or rx.dim() != 2 or not rx.is_cuda:
+            raise ValueError("rx must be a uint8 [B, W] device tensor")
+        rx = rx.contiguous()
+        B, W = rx.shape
+        ln = rx_len.to(device=rx.device, dtype=torch.int32).contiguous()
+        if ln.numel() != B:
+            raise ValueError("rx_len must have B entries")
+        info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=rx.device)
+        xh = torch.empty((c.n_words, B), dtype=torch.int32, device=rx.device) if want_xhat else None
+        rc = _lib.lib().pcub_sc_decode_deletion(_p(rx), _p(ln), B, W, c.n, self.n0, self.pd, _p(c.fmask_dev),
+                                                _p(c.fval_dev), c.K, _p(info), _p(xh), _stream())
+        _lib.check(rc, "pcub_sc_decode_deletion")
+        return info, xh
+
+    def decode(self, rx, rx_len):
+        """Returns (info [B, K] uint8, xhat [B, N] uint8) on device."""
+        info_w, xh_w = self.decode_native(rx, rx_len)
+        return unpack(info_w, self.code.K), unpack(xh_w, self.code.N)
+
+
+def pad_words(words, device=None):
+    """List of received words (0/1 sequences of varying length) -> ([B, W] uint8, [B] int32) on device."""
+    B = len(words)
+    W = max([len(w) for w in words] + [1])
+    a = np.zeros((B, W), np.uint8)
+    for b, w in enumerate(words):
+        a[b, :len(w)] = np.asarray(w, dtype=np.uint8)
+    dev = torch.device("cuda") if device is None else device
+    return (torch.from_numpy(a).to(dev), torch.tensor([len(w) for w in words], dtype=torch.int32, device=dev))

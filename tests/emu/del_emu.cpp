@@ -1,0 +1,151 @@
+// Host emulation of the deletion-channel decode (TEST ONLY).
+// Compiles polarcub_amd/csrc/trellis_body.h -- the trellis code the kernel runs --
+// for the CPU and drives it level-synchronously over the T trellises of a
+// codeword, with a scalar SC over the collapsed memoryless rows in natural order
+// (the kernel does that part with cross-lane XSub).  Not part of the product
+// library; nothing in polarcub_amd loads it.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "trellis_body.h"
+
+using namespace pcub;
+
+namespace {
+
+struct Ctx {
+    const uint32_t* fmask;
+    const uint32_t* fval;
+    int u;  // next u index
+    std::vector<int> info;
+};
+
+int fbit(const uint32_t* w, int i) { return (int)((w[i >> 5] >> (i & 31)) & 1u); }
+
+// SC over compact normalised values in natural order; returns the re-encoded vector.
+std::vector<int> mem_sc(const std::vector<double>& v, Ctx& cx) {
+    const size_t M = v.size();
+    if (M == 1) {
+        const int i = cx.u++;
+        if (fbit(cx.fmask, i)) return {fbit(cx.fval, i)};
+        const int d = (int)leaf_v(v[0]);
+        cx.info.push_back(d);
+        return {d};
+    }
+    std::vector<double> c(M / 2);
+    for (size_t h = 0; h < M / 2; ++h) c[h] = op_f(v[2 * h], v[2 * h + 1]);
+    const std::vector<int> xm = mem_sc(c, cx);
+    for (size_t h = 0; h < M / 2; ++h) c[h] = op_g(v[2 * h], v[2 * h + 1], (uint32_t)xm[h]);
+    const std::vector<int> xp = mem_sc(c, cx);
+    std::vector<int> x(M);
+    for (size_t h = 0; h < M / 2; ++h) {
+        x[2 * h] = xm[h] ^ xp[h];
+        x[2 * h + 1] = xp[h];
+    }
+    return x;
+}
+
+template <int L>
+struct Cap {
+    static constexpr int V = L / 2 + 1;
+    static constexpr int E0 = 3 * V;
+    static constexpr int E1 = 2 * V * V;
+};
+
+template <int L, int LEN>
+struct Node {
+    template <class PT>
+    static std::vector<uint32_t> run(const std::vector<PT>& ts, Ctx& cx) {
+        const size_t T = ts.size();
+        std::vector<uint32_t> out(T);
+        if constexpr (LEN == 2) {
+            Trel<1, Cap<L>::V, Cap<L>::E1> c;
+            std::vector<double> vals(T);
+            for (size_t t = 0; t < T; ++t) {
+                double m0, m1;
+                trellis_transform<2>(ts[t], c, nullptr);
+                trellis_marginal(c, m0, m1);
+                vals[t] = norm_pack(m0, m1);
+            }
+            const std::vector<int> xm = mem_sc(vals, cx);
+            for (size_t t = 0; t < T; ++t) {
+                double m0, m1;
+                const uint32_t d = (uint32_t)xm[t];
+                trellis_transform<2>(ts[t], c, &d);
+                trellis_marginal(c, m0, m1);
+                vals[t] = norm_pack(m0, m1);
+            }
+            const std::vector<int> xp = mem_sc(vals, cx);
+            for (size_t t = 0; t < T; ++t) out[t] = (uint32_t)((xm[t] ^ xp[t]) | (xp[t] << 1));
+        } else {
+            constexpr int H = LEN / 2;
+            using CT = Trel<H, Cap<L>::V, Cap<L>::E1>;
+            std::vector<CT> cs(T);
+            for (size_t t = 0; t < T; ++t) {
+                trellis_transform<LEN>(ts[t], cs[t], nullptr);
+                trellis_normalize<H>(cs[t]);
+            }
+            const std::vector<uint32_t> ym = Node<L, H>::run(cs, cx);
+            for (size_t t = 0; t < T; ++t) {
+                trellis_transform<LEN>(ts[t], cs[t], &ym[t]);
+                trellis_normalize<H>(cs[t]);
+            }
+            const std::vector<uint32_t> yp = Node<L, H>::run(cs, cx);
+            for (size_t t = 0; t < T; ++t) {
+                uint32_t x = 0;
+                for (int h = 0; h < H; ++h)
+                    x |= ((((ym[t] ^ yp[t]) >> h) & 1u) << (2 * h)) | (((yp[t] >> h) & 1u) << (2 * h + 1));
+                out[t] = x;
+            }
+        }
+        return out;
+    }
+};
+
+template <int N0>
+void decode_one(const uint8_t* w, int len, int n, double pd, Ctx& cx, std::vector<int>& xhat) {
+    constexpr int L = 1 << N0;
+    const int tb = n - N0;
+    const int T = 1 << tb;
+    auto bit = [w](int i) { return (int)w[i]; };
+    std::vector<Trel<L, Cap<L>::V, Cap<L>::E0>> base(T);
+    for (int t = 0; t < T; ++t) {
+        int s, m;
+        segment_of(bit, len, tb, t, s, m);
+        trellis_build<L>(base[t], bit, s, m, pd);
+    }
+    const std::vector<uint32_t> x = Node<L, L>::run(base, cx);
+    xhat.assign((size_t)T * L, 0);
+    for (int t = 0; t < T; ++t)
+        for (int i = 0; i < L; ++i) xhat[(size_t)t * L + i] = (int)((x[t] >> i) & 1u);
+}
+
+}  // namespace
+
+extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, long long B, int stride, int n, int n0,
+                                   double pd, const uint32_t* fmask, const uint32_t* fval, uint32_t* info,
+                                   uint32_t* xhat) {
+    const int N = 1 << n;
+    int K = 0;
+    for (int i = 0; i < N; ++i) K += 1 - fbit(fmask, i);
+    for (long long b = 0; b < B; ++b) {
+        Ctx cx{fmask, fval, 0, {}};
+        std::vector<int> xh;
+        const uint8_t* w = rx + b * (long long)stride;
+        const int len = rx_len[b];
+        switch (n0) {
+            case 1: decode_one<1>(w, len, n, pd, cx, xh); break;
+            case 2: decode_one<2>(w, len, n, pd, cx, xh); break;
+            case 3: decode_one<3>(w, len, n, pd, cx, xh); break;
+            default: return -1;
+        }
+        if ((int)cx.info.size() != K) return -2;
+        for (int i = 0; i < K; ++i)
+            if (cx.info[i]) info[(long long)(i >> 5) * B + b] |= 1u << (i & 31);
+        for (int i = 0; i < N; ++i)
+            if (xh[i]) xhat[(long long)(i >> 5) * B + b] |= 1u << (i & 31);
+    }
+    return 0;
+}

@@ -1,0 +1,130 @@
+"""Deletion-channel SC decode on the GPU (pcub_sc_decode_deletion) against the
+reference's golden vectors and the CPU oracle: info bits and x_hat bit-exact."""
+import contextlib
+import io
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import trellis_oracle as tro
+from tests.conftest import load_golden
+from tests.test_trellis_oracle import deletion_edge_cases
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sc():
+    from polarcub_amd import _lib, sc as m
+    _lib.lib()
+    return m
+
+
+def _dec(sc, n, n0, pd, frozen, fval, rx, rx_len):
+    code = sc.CodeSpec(1 << n, frozen, fval, device="cuda")
+    d = sc.DeletionDecoder(code, n0, pd)
+    info, xhat = d.decode(torch.from_numpy(np.ascontiguousarray(rx, np.uint8)).cuda(),
+                          torch.from_numpy(np.asarray(rx_len, np.int32)).cuda())
+    torch.cuda.synchronize()
+    return info.cpu().numpy(), xhat.cpu().numpy()
+
+
+def test_c5_golden(sc):
+    g = load_golden("deletion_n8")
+    m = g["meta"]
+    info, xhat = _dec(sc, m["n"], m["n0"], m["pd"], g["frozen"], g["fval"], g["rx"], g["rx_len"])
+    assert np.array_equal(info, g["info"])
+    assert np.array_equal(xhat, g["xhat"])
+
+
+@pytest.mark.parametrize("idx", range(11))
+def test_edge_golden(sc, idx):
+    c = deletion_edge_cases()[idx]
+    n, n0, ones = (int(v) for v in c["shape"])
+    if ones != 0 or not sc.deletion_supported(n, n0):
+        pytest.skip("outside the kernel's shapes (generic plugin path)")
+    info, xhat = _dec(sc, n, n0, float(c["pd"][0]), c["frozen"], c["fval"], c["rx"], c["rx_len"])
+    assert np.array_equal(info, c["info"])
+    assert np.array_equal(xhat, c["xhat"])
+
+
+SHAPES = [(n0, n0 + tb) for n0 in (1, 2, 3) for tb in range(1, 7)]
+
+
+@pytest.mark.parametrize("n0,n", SHAPES)
+def test_random_vs_oracle(sc, n0, n):
+    """Every kernel shape: channel outputs at several deletion rates plus adversarial words,
+    random frozen sets (incl. all-frozen and all-information windows) vs the oracle."""
+    N = 1 << n
+    rng = np.random.default_rng(1000 * n0 + n)
+    prng = random.Random(n)
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    frozen[: N // 4] = 1
+    frozen[-(N // 8) or -1:] = 0
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    pd = [0.05, 0.1, 0.3][n % 3]
+    words = []
+    for t in range(10):
+        x = [int(b) for b in rng.integers(0, 2, N)]
+        cw = tro.add_guard_bands(x, n, n0, 0.1)
+        words.append(tro.deletion_channel(cw, pd if t < 8 else 0.6, prng))
+    words += [[], [1], [0] * 9, [int(b) for b in rng.integers(0, 2, 3 * N)]]
+    W = max(len(w) for w in words)
+    rx = np.zeros((len(words), W), np.uint8)
+    for i, w in enumerate(words):
+        rx[i, :len(w)] = w
+    info, xhat = _dec(sc, n, n0, pd, frozen, fval, rx, [len(w) for w in words])
+    for i, w in enumerate(words):
+        x_ref, i_ref = tro.decode_deletion(w, n, n0, pd, frozen, fval)
+        assert list(info[i]) == i_ref, (i, w)
+        assert list(xhat[i]) == x_ref, (i, w)
+
+
+def test_ragged_batches_match_single(sc):
+    """A large batch (padding groups in the last workgroup) equals per-codeword results."""
+    g = load_golden("deletion_n8")
+    m = g["meta"]
+    reps = np.concatenate([np.arange(g["rx"].shape[0])] * 7)[:301]
+    info, xhat = _dec(sc, m["n"], m["n0"], m["pd"], g["frozen"], g["fval"], g["rx"][reps], g["rx_len"][reps])
+    assert np.array_equal(info, g["info"][reps])
+    assert np.array_equal(xhat, g["xhat"][reps])
+
+
+def test_facade_dispatch_and_mc_line():
+    """BinaryPolarEncoderDecoder.decode on a received-word collection runs the kernel (the
+    trellises are never built on the host) and encodeDecodeSimulation with the
+    main_deletion.py closures prints the reference's line."""
+    from polarcub_amd import coding, deletion, vectors
+    g = load_golden("deletion_n8")
+    m = g["meta"]
+    n, n0, pd, xi = m["n"], m["n0"], m["pd"], m["xi"]
+    N = 1 << n
+    enc = coding.BinaryPolarEncoderDecoder(N, set(int(i) for i in np.nonzero(g["frozen"])[0]), m["crs"])
+    xvd = vectors.BinaryMemorylessVectorDistribution(N)
+    xvd.probs[:] = 0.5
+    for t in range(4):
+        w = list(map(int, g["rx"][t, :g["rx_len"][t]]))
+        coll = deletion.buildCollectionOfBinaryTrellises_uniformInput_deletion(w, pd, xi, n, n0, 0)
+        x, info = enc.decode(xvd, coll)
+        assert coll._lazy is not None, "host trellises were built: the kernel path did not run"
+        assert np.array_equal(info, g["info"][t]) and np.array_equal(x, g["xhat"][t])
+
+    frozen = set(int(i) for i in np.nonzero(g["genie_frozen"])[0])
+    crng = random.Random()
+    crng.seed(m["channel_seed"])
+
+    def make_x():
+        v = vectors.BinaryMemorylessVectorDistribution(N)
+        v.probs[:] = 0.5
+        return v
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        coding.encodeDecodeSimulation(
+            N, make_x, lambda e: deletion.addDeletionGuardBands(e, n, n0, xi, 0),
+            lambda c: deletion.deletionChannelSimulation(c, pd, None, crng),
+            lambda r: deletion.buildCollectionOfBinaryTrellises_uniformInput_deletion(r, pd, xi, n, n0, 0),
+            m["mc_trials"], frozen, commonRandomnessSeed=m["crs"], randomInformationSeed=m["info_seed"])
+    assert buf.getvalue().strip().splitlines()[-1] == m["line"]

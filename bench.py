@@ -1,22 +1,26 @@
 #!/usr/bin/env python3
-"""Throughput benchmark: decoded codewords/s, binary SC, N=1024 rate-1/2 BI-AWGN.
+"""Throughput benchmark: decoded codewords/s of the SC decoder on MI355X.
 
-BASELINE.json metric: "decoded codewords/sec at N=1024 BI-AWGN, batch=1M; FER
-match vs reference".  Workload = BASELINE.json configs[1]: N=1024, K=512,
-Eb/N0 = 2 dB, batch 2^20 codewords per GPU (weak scaling), synthetic data
-generated on the device (Philox via torch.randn) and resident in HBM before the
-timed region.  One step = one pcub_sc_decode_bin launch over the whole batch
-(joint-probability pairs in -> packed info bits + packed x_hat out).
+BASELINE.json metric: "decoded codewords/sec at N=1024 BI-AWGN, batch=1M; FER match
+vs reference".  Default workload = BASELINE.json configs[1]: binary SC, N=1024,
+K=512, Eb/N0 = 2 dB, 2^20 codewords per GPU (weak scaling).  Other configs as
+--workload (reported beside it, not the headline):
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 10] [--batch 1048576]
+  awgn      configs[1] (N=1024) / configs[2] with --n 12 (N=4096)
+  deletion  configs[4]: main_deletion.py defaults, n=8, n0=2, pd=0.1, xi=0.1
+  qary      configs[3]: q=4, N=256, QSC(0.11)
 
-Multi-GPU: launched by torch.distributed.run, one rank per GPU; each rank
-decodes its own batch (no data-path collective); one RCCL all_reduce of the
-error counters and a max-reduce of the elapsed time at the end.
+Synthetic data is generated on the device (torch Philox), resident in HBM before the
+timed region.  One step = one decode launch over the whole per-GPU batch.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload awgn|deletion|qary] [--batch B]
+
+Multi-GPU: launched by torch.distributed.run, one rank per GPU; rank r decodes its
+own batch (global codewords [r*B, (r+1)*B), no data-path collective); one RCCL
+all_reduce of the error counters and a max-reduce of the elapsed time at the end.
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -28,7 +32,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from polarcub_amd import channel, construction, sc  # noqa: E402
+from polarcub_amd import channel, construction, mc, sc  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -37,30 +41,20 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_inputs(code, B, sigma2, seed, device, chunk=1 << 18):
-    """Random info bits -> GPU encoder -> BI-AWGN joint pairs in native [N, B, 2] layout."""
-    gen = torch.Generator(device=device)
-    gen.manual_seed(seed)
-    xy = torch.empty((code.N, B, 2), dtype=torch.float64, device=device)
-    info = torch.empty((B, code.K), dtype=torch.uint8, device=device)
-    for b0 in range(0, B, chunk):
-        b1 = min(B, b0 + chunk)
-        inf = torch.randint(0, 2, (b1 - b0, code.K), dtype=torch.uint8, device=device, generator=gen)
-        info[b0:b1] = inf
-        xw = sc.encode_native(code, sc.pack(inf))
-        x_nb = channel.bits_from_words(xw, code.N)
-        channel.awgn_pairs_native(x_nb, sigma2, generator=gen, out=xy[:, b0:b1, :])
-        del xw, x_nb
-    return xy, info
+def host_cores():
+    try:
+        c = len(os.sched_getaffinity(0))
+    except AttributeError:
+        c = os.cpu_count() or 1
+    return max(1, min(c, 16))
 
 
-def measured_traffic(variant, n, batch):
-    """Per-launch HBM bytes of this exact decode configuration from the committed
-    rocprofv3 PMC passes (profiles/<round>/bin_v<variant>_n<n>/summary.json, written by
-    scripts/collect_profiles.py; FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
+def measured_traffic(tag, batch):
+    """Per-launch HBM bytes of this exact configuration from the committed rocprofv3 PMC
+    passes (profiles/<round>/<tag>/summary.json, written by scripts/collect_profiles.py:
+    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or (None, None)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "bin_v%d_n%d" % (variant, n), "summary.json")),
-                       reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", tag, "summary.json")), reverse=True):
         with open(path) as f:
             s = json.load(f)
         if s.get("batch") == batch and "traffic_bytes" in s:
@@ -68,38 +62,217 @@ def measured_traffic(variant, n, batch):
     return None, None
 
 
-def cpu_baseline(code, xy_native, seconds_target=12.0):
-    """The C oracle (oracle/sc_oracle.c, -O2 -ffp-contract=off) on the host cores, on a
-    bounded sample of the same synthetic codewords (rank 0 only)."""
-    from concurrent.futures import ThreadPoolExecutor
+# ----------------------------------------------------------------------------- workloads
 
-    from oracle import orc
-    orc.lib()
-    ncw = 4096
-    sample = xy_native[:, :ncw, :].permute(1, 0, 2).contiguous().cpu().numpy()  # [ncw, N, 2]
-    t0 = time.perf_counter()
-    orc.decode_bin(sample[:64], code.frozen_mask, code.frozen_values)
-    per_cw = (time.perf_counter() - t0) / 64
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    reps = max(1, int(round(seconds_target / (per_cw * ncw))))
+class Awgn:
+    """Binary SC over BI-AWGN (configs[1], configs[2] with --n 12)."""
+    kernel = "k_sc_bin"
 
-    def work(i):
-        part = sample[(i * ncw) // cores:((i + 1) * ncw) // cores]
-        for _ in range(reps):
-            orc.decode_bin(part, code.frozen_mask, code.frozen_values)
-        return part.shape[0] * reps
+    def __init__(self, a, device, rank):
+        self.a = a
+        n, N = a.n, 1 << a.n
+        K = int(round(N * a.rate))
+        self.n, self.N, self.K, self.B = n, N, K, a.batch
+        self.sigma2 = construction.awgn_sigma2(a.ebn0, K / N)
+        frozen = construction.bhattacharyya_frozen(n, K, self.sigma2)
+        self.code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(frozen)[0].tolist()), 1, device=device)
+        sc.set_variant(a.variant)
+        self.variant = sc.default_variant() if a.variant is None else a.variant
+        sc.set_max_blocks_per_cu(a.max_blocks)
+        self.dec = sc.BinaryDecoder(self.code)
+        gen = torch.Generator(device=device)
+        gen.manual_seed(mc.shard_seed(a.seed, rank))
+        self.xy, self.info_tx = mc.awgn_batch(self.code, self.B, self.sigma2, gen)
+        self.outs = (torch.empty((self.code.info_words, self.B), dtype=torch.int32, device=device),
+                     None if a.no_xhat else torch.empty((self.code.n_words, self.B), dtype=torch.int32, device=device),
+                     None)
+        self.dec.workspace(self.B)
 
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(cores) as ex:
-        total = sum(ex.map(work, range(cores)))
-    dt = time.perf_counter() - t0
-    return {"value": total / dt, "unit": "codewords/s", "cores": cores, "kind": "port",
-            "sample": "%d codewords x %d passes of the bench's own synthetic N=%d inputs, "
-                      "oracle/sc_oracle.c on %d threads (%.1f CPU-s)" % (ncw, reps, code.N, cores, dt * cores)}
+    def step(self):
+        self.dec.decode_native(self.xy, out=self.outs)
+
+    def errors(self):
+        d = sc.unpack(self.outs[0], self.K)
+        return mc.error_counts(d, self.info_tx)
+
+    def bytes_alg(self):
+        return 16 * self.N + self.N // 8 + self.K // 8  # f64 pairs in + packed x_hat + packed info
+
+    def tag(self):
+        return "bin_v%d_n%d" % (self.variant, self.n)
+
+    def describe(self, world):
+        a = self.a
+        return dict(
+            metric="decoded codewords/sec at N=%d BI-AWGN, batch=%d per GPU; FER match vs reference" % (self.N, self.B),
+            dtype="f64",
+            data="synthetic: uniform info bits, GPU polar encoder, BI-AWGN Eb/N0=%.1f dB pairs generated on device"
+                 % a.ebn0,
+            config={"workload": "binary SC decode N=%d K=%d BI-AWGN %.1f dB (BASELINE configs[%d])"
+                                % (self.N, self.K, a.ebn0, 1 if self.n == 10 else 2),
+                    "N": self.N, "K": self.K, "batch_per_gpu": self.B, "ebn0_db": a.ebn0,
+                    "kernel_variant": self.variant, "max_blocks_per_cu": a.max_blocks,
+                    "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
+
+    def cpu_baseline(self, seconds=12.0):
+        """oracle/sc_oracle.c (-O2 -ffp-contract=off) on the host cores, threads over a bounded
+        sample of the bench's own codewords."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle import orc
+        orc.lib()
+        code, ncw = self.code, 4096
+        sample = self.xy[:, :ncw, :].permute(1, 0, 2).contiguous().cpu().numpy()
+        t0 = time.perf_counter()
+        orc.decode_bin(sample[:64], code.frozen_mask, code.frozen_values)
+        per_cw = (time.perf_counter() - t0) / 64
+        cores = host_cores()
+        reps = max(1, int(round(seconds / (per_cw * ncw))))
+
+        def work(i):
+            part = sample[(i * ncw) // cores:((i + 1) * ncw) // cores]
+            for _ in range(reps):
+                orc.decode_bin(part, code.frozen_mask, code.frozen_values)
+            return part.shape[0] * reps
+
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(cores) as ex:
+            total = sum(ex.map(work, range(cores)))
+        dt = time.perf_counter() - t0
+        return {"value": total / dt, "unit": "codewords/s", "cores": cores, "kind": "port",
+                "sample": "%d codewords x %d passes of the bench's own synthetic N=%d inputs, oracle/sc_oracle.c "
+                          "on %d threads (%.1f CPU-s)" % (ncw, reps, code.N, cores, dt * cores)}
+
+
+class Deletion:
+    """Deletion channel, main_deletion.py defaults (configs[4]): n=8, n0=2, pd=0.1, xi=0.1.
+    Frozen set: the N/4 most reliable indices by the reference's genie ranking (fixture)."""
+    kernel = "k_sc_del"
+
+    def __init__(self, a, device, rank):
+        self.a = a
+        self.n, self.n0, self.pd, self.xi = a.n if a.n != 10 else 8, a.n0, a.pd, a.xi
+        self.N = 1 << self.n
+        self.B = a.batch
+        g = np.load(os.path.join(ROOT, "tests", "golden", "deletion_n8.npz"), allow_pickle=False)
+        if self.n == 8:
+            score = g["genie_score"]
+            order = sorted(range(self.N), key=lambda i: (score[i], i))
+            frozen = set(order[self.N // 4:])
+        else:
+            frozen = set(np.nonzero(construction.bhattacharyya_frozen(self.n, self.N // 4, 0.5))[0].tolist())
+        self.code = sc.CodeSpec.from_frozen_set(self.N, frozen, 200, device=device)
+        self.K = self.code.K
+        self.dec = sc.DeletionDecoder(self.code, self.n0, self.pd)
+        gen = torch.Generator(device=device)
+        gen.manual_seed(mc.shard_seed(a.seed, rank))
+        self.rx, self.rx_len, self.info_tx = mc.deletion_batch(self.code, self.B, self.n0, self.xi, self.pd, gen)
+        self.outs = None
+
+    def step(self):
+        self.outs = self.dec.decode_native(self.rx, self.rx_len)
+
+    def errors(self):
+        return mc.error_counts(sc.unpack(self.outs[0], self.K), self.info_tx)
+
+    def bytes_alg(self):
+        return float(self.rx_len.float().mean().item()) + 4 + self.N // 8 + self.K // 8
+
+    def tag(self):
+        return "del_n%d_n0%d" % (self.n, self.n0)
+
+    def describe(self, world):
+        return dict(
+            metric="decoded codewords/sec, deletion channel N=%d n0=%d pd=%.2f (main_deletion.py), batch=%d per GPU"
+                   % (self.N, self.n0, self.pd, self.B),
+            dtype="f64",
+            data="synthetic: uniform info bits, GPU polar encoder, guard bands (xi=%.2f), deletions drawn on device"
+                 % self.xi,
+            config={"workload": "deletion SC decode N=%d n0=%d K=%d pd=%.2f (BASELINE configs[4])"
+                                % (self.N, self.n0, self.K, self.pd),
+                    "N": self.N, "K": self.K, "n0": self.n0, "pd": self.pd, "xi": self.xi, "batch_per_gpu": self.B,
+                    "received_len_mean": float(self.rx_len.float().mean().item()),
+                    "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
+
+    def cpu_baseline(self, seconds=10.0):
+        """oracle/trellis_oracle.py (pure Python restatement, one thread) on a bounded sample."""
+        from oracle import trellis_oracle as tro
+        rx = self.rx[:4096].cpu().numpy()
+        ln = self.rx_len[:4096].cpu().numpy()
+        fm, fv = self.code.frozen_mask, self.code.frozen_values
+        t0 = time.perf_counter()
+        done = 0
+        while time.perf_counter() - t0 < seconds and done < rx.shape[0]:
+            tro.decode_deletion(list(map(int, rx[done, :ln[done]])), self.n, self.n0, self.pd, fm, fv)
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "codewords/s", "cores": 1, "kind": "port",
+                "sample": "first %d codewords of the bench's own received words, oracle/trellis_oracle.py "
+                          "(pure Python, 1 thread, %.1f s)" % (done, dt)}
+
+
+class Qary:
+    """q-ary SC (configs[3]): q=4, N=256, K=128, QSC(p)."""
+    kernel = "k_sc_qary"
+
+    def __init__(self, a, device, rank):
+        self.a = a
+        self.q, self.n = a.q, (a.n if a.n != 10 else 8)
+        self.N = 1 << self.n
+        self.K = self.N // 2
+        self.B = a.batch
+        z = construction.bhattacharyya_z(self.n, 0.5)
+        order = sorted(range(self.N), key=lambda i: (z[i], i))
+        mask = np.ones(self.N, np.uint8)
+        mask[order[:self.K]] = 0
+        self.code = sc.QaryCode(self.q, self.N, mask, device=device)
+        self.dec = sc.QaryDecoder(self.code)
+        gen = torch.Generator(device=device)
+        gen.manual_seed(mc.shard_seed(a.seed, rank))
+        self.xy, self.info_tx = mc.qsc_batch(self.code, self.B, a.qsc_p, gen)
+        self.dec.workspace(self.B)
+        self.outs = None
+
+    def step(self):
+        self.outs = self.dec.decode_native(self.xy)
+
+    def errors(self):
+        return mc.error_counts(self.outs[0].t(), self.info_tx)
+
+    def bytes_alg(self):
+        bits = max(1, (self.q - 1).bit_length())
+        return 8 * self.q * self.N + (self.N * bits) // 8 + (self.K * bits) // 8
+
+    def tag(self):
+        return "qary_q%d_n%d" % (self.q, self.n)
+
+    def describe(self, world):
+        return dict(
+            metric="decoded codewords/sec, q=%d SC N=%d QSC(%.2f), batch=%d per GPU" % (self.q, self.N, self.a.qsc_p,
+                                                                                     self.B),
+            dtype="f64",
+            data="synthetic: uniform info symbols, GPU q-ary encoder, QSC(%.2f) on device" % self.a.qsc_p,
+            config={"workload": "q-ary SC decode q=%d N=%d K=%d QSC(%.2f) (BASELINE configs[3])"
+                                % (self.q, self.N, self.K, self.a.qsc_p),
+                    "N": self.N, "K": self.K, "q": self.q, "batch_per_gpu": self.B,
+                    "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
+
+    def cpu_baseline(self, seconds=10.0):
+        from oracle import orc
+        orc.lib()
+        ncw = 2048
+        sample = self.xy[:, :ncw, :].permute(1, 0, 2).contiguous().cpu().numpy()
+        t0 = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t0 < seconds:
+            orc.decode_qary(self.q, sample, self.code.frozen_mask)
+            reps += 1
+        dt = time.perf_counter() - t0
+        return {"value": ncw * reps / dt, "unit": "codewords/s", "cores": 1, "kind": "port",
+                "sample": "%d codewords x %d passes, oracle/sc_oracle.c q-ary, 1 thread" % (ncw, reps)}
+
+
+WORKLOADS = {"awgn": Awgn, "deletion": Deletion, "qary": Qary}
 
 
 def main():
@@ -107,110 +280,89 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=10, help="log2 code length")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="awgn")
+    ap.add_argument("--n", type=int, default=10, help="log2 code length (awgn; deletion/qary default 8)")
     ap.add_argument("--rate", type=float, default=0.5)
     ap.add_argument("--ebn0", type=float, default=2.0)
+    ap.add_argument("--n0", type=int, default=2, help="deletion: log2 inputs per trellis")
+    ap.add_argument("--pd", type=float, default=0.1, help="deletion probability")
+    ap.add_argument("--xi", type=float, default=0.1, help="guard-band parameter")
+    ap.add_argument("--q", type=int, default=4)
+    ap.add_argument("--qsc-p", type=float, default=0.11)
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU")
-    ap.add_argument("--variant", type=int, default=None, help="decode kernel variant (default: the library's)")
+    ap.add_argument("--variant", type=int, default=None, help="binary decode kernel variant (default: the library's)")
     ap.add_argument("--max-blocks", type=int, default=0, help="cap decode workgroups per CU (0 = occupancy)")
     ap.add_argument("--seed", type=int, default=20250204)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-xhat", action="store_true")
-    args = ap.parse_args()
+    a = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = mc.dist_env()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(device)
 
-    n, N = args.n, 1 << args.n
-    K = int(round(N * args.rate))
-    sigma2 = construction.awgn_sigma2(args.ebn0, K / N)
-    frozen = construction.bhattacharyya_frozen(n, K, sigma2)
-    code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(frozen)[0].tolist()), 1, device=device)
-    sc.set_variant(args.variant)
-    variant = sc.default_variant() if args.variant is None else args.variant
-    sc.set_max_blocks_per_cu(args.max_blocks)
-    dec = sc.BinaryDecoder(code)
-    B = args.batch
-
     t0 = time.time()
-    xy, info_tx = make_inputs(code, B, sigma2, args.seed + 7919 * rank, device)
+    w = WORKLOADS[a.workload](a, device, rank)
     torch.cuda.synchronize()
-    log("rank %d: inputs %.1f GB generated in %.1f s" % (rank, xy.numel() * 8 / 1e9, time.time() - t0))
-    outs = (torch.empty((code.info_words, B), dtype=torch.int32, device=device),
-            None if args.no_xhat else torch.empty((code.n_words, B), dtype=torch.int32, device=device), None)
-    dec.workspace(B)
+    log("rank %d: %s inputs for %d codewords generated in %.1f s" % (rank, a.workload, w.B, time.time() - t0))
 
-    for _ in range(args.warmup):
-        dec.decode_native(xy, out=outs)
+    for _ in range(a.warmup):
+        w.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     t_start = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(a.steps):
         evs[i][0].record(stream)
-        dec.decode_native(xy, out=outs)
+        w.step()
         evs[i][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    kern_ms = [x.elapsed_time(y) for x, y in evs]
 
-    # frame errors of the last decode (identical each step)
-    info_dec = sc.unpack(outs[0], K)
-    errs = (info_dec != info_tx).any(dim=1)
-    counters = torch.tensor([B, int(errs.sum().item()), int((info_dec != info_tx).sum().item()), 0],
-                            dtype=torch.int64, device=device)
-    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-    total_cw = int(counters[0].item()) * args.steps
+    fe, be = w.errors()  # of the last decode (identical every step)
+    counters, elapsed = mc.reduce_counters([w.B, fe, be, 0], elapsed, device if world > 1 else None)
+    total_cw = counters[0] * a.steps
     value = total_cw / elapsed
-    ms_per_step = elapsed * 1e3 / args.steps
 
     if rank == 0:
         avg_kern_s = float(np.mean(kern_ms)) / 1e3
-        b_alg = 16 * N + N // 8 + K // 8  # f64 pairs in + packed x_hat + packed info, per codeword
-        achieved = b_alg * B / avg_kern_s / 1e9
-        traffic, traffic_src = measured_traffic(variant, n, B)
+        b_alg = w.bytes_alg()
+        achieved = b_alg * w.B / avg_kern_s / 1e9
+        traffic, traffic_src = measured_traffic(w.tag(), w.B)
+        d = w.describe(world)
         rec = {
-            "metric": "decoded codewords/sec at N=%d BI-AWGN, batch=%d per GPU; FER match vs reference" % (N, B),
+            "metric": d["metric"],
             "value": value,
             "unit": "codewords/s",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed * 1e3 / a.steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic: uniform info bits, GPU polar encoder, BI-AWGN Eb/N0=%.1f dB pairs generated on device" % args.ebn0,
-            "config": {"workload": "binary SC decode N=%d K=%d BI-AWGN %.1f dB (BASELINE configs[1])" % (N, K, args.ebn0),
-                       "N": N, "K": K, "batch_per_gpu": B, "ebn0_db": args.ebn0, "kernel_variant": variant, "max_blocks_per_cu": args.max_blocks,
-                       "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world},
-            "fer": float(counters[1].item()) / int(counters[0].item()),
-            "frame_errors": int(counters[1].item()),
+            "dtype": d["dtype"],
+            "data": d["data"],
+            "config": d["config"],
+            "fer": counters[1] / counters[0],
+            "frame_errors": counters[1],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "k_sc_bin", "kernel_ms": float(np.mean(kern_ms)),
-                         "bytes_alg_per_cw": b_alg},
+                         "kernel": w.kernel, "kernel_ms": float(np.mean(kern_ms)), "bytes_alg_per_cw": b_alg},
         }
-        if world == 1 and not args.no_cpu:
-            rec["cpu_baseline"] = cpu_baseline(code, xy)
+        if world == 1 and not a.no_cpu:
+            rec["cpu_baseline"] = w.cpu_baseline()
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

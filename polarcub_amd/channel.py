@@ -31,3 +31,46 @@ def awgn_pairs_native(x_nb, sigma2, generator=None, out=None):
     out[:, :, 0] = c * torch.exp(-((y - 1.0) ** 2) / (2.0 * sigma2))
     out[:, :, 1] = c * torch.exp(-((y + 1.0) ** 2) / (2.0 * sigma2))
     return out
+
+
+def guard_band_positions(n, n0, xi, ones=0):
+    """Positions of the N codeword bits inside the guard-banded word of
+    Guardbands.addDeletionGuardBands (Guardbands.py:4-44), and its length."""
+    from .deletion import addDeletionGuardBands
+    N = 1 << n
+    marked = addDeletionGuardBands([i + 2 for i in range(N)], n, n0, xi, ones)
+    pos = [j for j, v in enumerate(marked) if v >= 2]
+    assert len(pos) == N
+    return pos, len(marked), [j for j, v in enumerate(marked) if v == 1]
+
+
+def deletion_words(x_bn, n, n0, xi, pd, generator=None):
+    """x_bn: [B, N] 0/1 codewords (device) -> guard bands added, every symbol deleted
+    independently with probability pd (BinaryTrellis.deletionChannelSimulation's law, drawn
+    with torch's Philox instead of MT19937), survivors packed to the left.
+    Returns (rx [B, W] uint8, rx_len [B] int32), W = guard-banded length."""
+    B, N = x_bn.shape
+    pos, W, ones_pos = guard_band_positions(n, n0, xi)
+    dev = x_bn.device
+    cw = torch.zeros((B, W), dtype=torch.uint8, device=dev)
+    cw[:, torch.tensor(pos, device=dev)] = x_bn.to(torch.uint8)
+    keep = torch.rand((B, W), device=dev, generator=generator) >= pd
+    dest = torch.cumsum(keep, dim=1, dtype=torch.int32) - 1
+    dest = torch.where(keep, dest, torch.full_like(dest, W))  # deleted symbols go to a trash column
+    rx = torch.zeros((B, W + 1), dtype=torch.uint8, device=dev)
+    rx.scatter_(1, dest.to(torch.int64), cw)
+    return rx[:, :W].contiguous(), keep.sum(dim=1, dtype=torch.int32)
+
+
+def qsc_pairs_native(x_nb, q, p, generator=None):
+    """x_nb: [N, B] symbols in [0, q) -> q-ary symmetric channel output y and the joint table
+    rows probs[y][x] (1-p if x == y else p/(q-1), ScalarDistributions/QaryMemorylessDistribution.py:780-784)
+    as [N, B, q] float64."""
+    N, B = x_nb.shape
+    dev = x_nb.device
+    err = torch.rand((N, B), device=dev, generator=generator, dtype=torch.float64) < p
+    shift = torch.randint(1, q, (N, B), device=dev, generator=generator)
+    y = torch.where(err, (x_nb.to(torch.int64) + shift) % q, x_nb.to(torch.int64))
+    hit = y.unsqueeze(-1) == torch.arange(q, device=dev)
+    return torch.where(hit, torch.tensor(1.0 - p, dtype=torch.float64, device=dev),
+                       torch.tensor(p / (q - 1), dtype=torch.float64, device=dev))

@@ -14,47 +14,13 @@
 #include <hip/hip_runtime.h>
 
 #include "polarcub_sc.h"
-#include "sc_bin_body.h"
+#include "sc_bin_kern.h"
 
 using namespace pcub;
 
 namespace {
 
-constexpr int kBlock = 256;
-
-// Decode kernel variants: virtual register subtree S (values per lane), lanes
-// per codeword G, and the minimum waves/SIMD the register allocation must allow.
-// Variant fields: S = register subtree values per lane, G = lanes per codeword,
-// W = minimum waves/SIMD for register allocation, L = deepest stage level in
-// LDS, T = non-temporal loads for the (once-streamed) input rows.
-struct Variant {
-    int S, G, W, L, T;
-};
-constexpr int kNumVariants = 19;
-constexpr Variant kVar[kNumVariants] = {
-    {16, 1, 2, 0, 0}, {8, 1, 4, 0, 0}, {32, 1, 1, 0, 0}, {16, 4, 2, 0, 0}, {8, 4, 4, 0, 0}, {16, 2, 2, 0, 0},
-    {32, 2, 1, 0, 0}, {8, 8, 4, 0, 0}, {16, 2, 2, 0, 1}, {8, 8, 4, 0, 1}, {16, 4, 2, 0, 1}, {8, 4, 4, 1, 0},
-    {16, 2, 4, 0, 1}, {16, 4, 4, 0, 1}, {8, 4, 4, 0, 1}, {32, 4, 2, 0, 1}, {32, 2, 2, 0, 1},
-    {32, 4, 3, 0, 1}, {32, 2, 3, 0, 1},
-};
-
-size_t lds_bytes(int v) { return kVar[v].L ? (size_t)kVar[v].S * kBlock * sizeof(double2) : 0; }
-
-template <int S, int G, int W, bool LDS, int NT>
-__global__ __launch_bounds__(kBlock, W) void k_sc_bin(BinArgs A) {
-    extern __shared__ double2 lds_last[];  // [S pairs][kBlock] when LDS (plus occupancy padding)
-    constexpr int CWB = kBlock / G;  // codewords per workgroup tile
-    const long long slot = (long long)blockIdx.x * kBlock + threadIdx.x;
-    const int j = threadIdx.x & (G - 1);
-    const int lane = threadIdx.x & 63;
-    const Lvl last = LDS ? Lvl{lds_last + threadIdx.x, kBlock} : Lvl{nullptr, 0};
-    const long long ntiles = (A.B + CWB - 1) / CWB;
-    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const long long cw = t * CWB + threadIdx.x / G;
-        const bool valid = cw < A.B;
-        decode_codeword<S, G, LDS, NT>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last);
-    }
-}
+constexpr int kBlock = kBinBlock;
 
 // rate-0 table: one byte per register subtree (first_frozen_depth)
 __global__ __launch_bounds__(kBlock) void k_ef_table(const uint32_t* fmask, int D, int SU, uint8_t* ef) {
@@ -68,29 +34,12 @@ __global__ __launch_bounds__(kBlock) void k_sc_bin_small(BinArgs A) {
     if (cw < A.B) decode_small<NN>(A, cw, true);
 }
 
-typedef void (*KernFn)(BinArgs);
+typedef BinKernFn KernFn;
 KernFn variant_kernel(int v) {
-    switch (v) {
-        case 1: return k_sc_bin<8, 1, 4, false, 0>;
-        case 2: return k_sc_bin<32, 1, 1, false, 0>;
-        case 3: return k_sc_bin<16, 4, 2, false, 0>;
-        case 4: return k_sc_bin<8, 4, 4, false, 0>;
-        case 5: return k_sc_bin<16, 2, 2, false, 0>;
-        case 6: return k_sc_bin<32, 2, 1, false, 0>;
-        case 7: return k_sc_bin<8, 8, 4, false, 0>;
-        case 8: return k_sc_bin<16, 2, 2, false, 1>;
-        case 9: return k_sc_bin<8, 8, 4, false, 1>;
-        case 10: return k_sc_bin<16, 4, 2, false, 1>;
-        case 11: return k_sc_bin<8, 4, 4, true, 0>;
-        case 12: return k_sc_bin<16, 2, 4, false, 1>;
-        case 13: return k_sc_bin<16, 4, 4, false, 1>;
-        case 14: return k_sc_bin<8, 4, 4, false, 1>;
-        case 15: return k_sc_bin<32, 4, 2, false, 1>;
-        case 16: return k_sc_bin<32, 2, 2, false, 1>;
-        case 17: return k_sc_bin<32, 4, 3, false, 1>;
-        case 18: return k_sc_bin<32, 2, 3, false, 1>;
-        default: return k_sc_bin<16, 1, 2, false, 0>;
-    }
+    if (KernFn k = bin_kernel_part0(v)) return k;
+    if (KernFn k = bin_kernel_part1(v)) return k;
+    if (KernFn k = bin_kernel_part2(v)) return k;
+    return bin_kernel_part3(v);
 }
 
 // {32, 4, 3, NT}: fastest at N=1024 on MI355X (profiles/r1/sweep_*.txt)
@@ -101,7 +50,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 
 // dynamic LDS for variant v: its stage level plus padding that caps residency at g_max_blocks
 size_t launch_lds(int v) {
-    size_t b = lds_bytes(v);
+    size_t b = bin_lds_bytes(v);
     if (g_max_blocks > 0) {
         const size_t cap = kLdsPerCu / (size_t)g_max_blocks;
         if (cap > b) b = cap - 256;
@@ -125,7 +74,7 @@ DevInfo dev_info() {
     if (hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return DevInfo{};
     for (int v = 0; v < kNumVariants; ++v) {
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, variant_kernel(v), kBlock, lds_bytes(v)) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, variant_kernel(v), kBlock, bin_lds_bytes(v)) != hipSuccess ||
             occ < 1)
             occ = 1;
         d.occ[v] = occ;

@@ -403,59 +403,75 @@ PCUB_HD void dispatch_final(const Chain& c, Lvl l1, double* v, bool fg, bool roo
 // G lanes (`lane` = wave lane id, for the exchanges) in scratch slot `slot`.
 // S = virtual register subtree (values per lane) in {8, 16, 32}; requires
 // N >= 2*S*G and N >= 32*G.  `store` is false for padding codewords.
-// A register subtree's u decisions and frozen bits as NW 64-bit windows (a
-// subtree of more than 64 real positions is split at its top node, each half
-// into its own window).
-template <int S, int G>
-struct SubWin {
-    static constexpr int SU = S * G;
-    static constexpr int NW = SU > 64 ? 2 : 1;
-    static constexpr int SUW = SU > 64 ? 64 : SU;  // bits per window
-    static constexpr uint64_t WMASK = (SUW == 64) ? ~0ull : ((1ull << SUW) - 1ull);
-    static_assert(SU <= 128, "at most two windows");
-
-    // decisions of the subtree from its S level-D values
+//
+// A register subtree's u decisions and frozen bits live in NW 64-bit windows
+// (NW = S*G/64 when the subtree has more than 64 real positions): WinTree splits
+// the subtree at its top nodes until each part is one window.
+template <int L, int G, int NWIN>
+struct WinTree {
     static PCUB_HD uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm, const uint64_t* fv, int lane) {
-        if constexpr (NW == 1) {
-            return SubV<S, 0, G>::run(v, ub[0], fm[0], fv[0], lane);
+        if constexpr (NWIN == 1) {
+            return SubV<L, 0, G>::run(v, ub[0], fm[0], fv[0], lane);
         } else {
-            constexpr int H = S / 2;
-            const int j = lane & (G - 1);
+            constexpr int H = L / 2;
+            constexpr int HW = NWIN / 2;
             double c[H];
             uint32_t ym, yp;
-            if (all_frozen<64>(fm[0], 0)) {
-                ym = frozen_local<H, G>(fv[0], j);
-                ub[0] = fv[0];
+            if (frozen_windows(fm)) {
+                ym = WinTree<H, G, HW>::frozen(ub, fv, lane & (G - 1));
             } else {
 #pragma unroll
                 for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
-                ym = SubV<H, 0, G>::run(c, ub[0], fm[0], fv[0], lane);
+                ym = WinTree<H, G, HW>::run(c, ub, fm, fv, lane);
             }
-            if (all_frozen<64>(fm[1], 0)) {
-                yp = frozen_local<H, G>(fv[1], j);
-                ub[1] = fv[1];
+            if (frozen_windows(fm + HW)) {
+                yp = WinTree<H, G, HW>::frozen(ub + HW, fv + HW, lane & (G - 1));
             } else {
 #pragma unroll
                 for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
-                yp = SubV<H, 0, G>::run(c, ub[1], fm[1], fv[1], lane);
+                yp = WinTree<H, G, HW>::run(c, ub + HW, fm + HW, fv + HW, lane);
             }
             return (ym ^ yp) | (yp << H);
         }
+    }
+
+    // NWIN/2 full windows all frozen (the half is rate-0)
+    static PCUB_HD bool frozen_windows(const uint64_t* fm) {
+        bool all = true;
+#pragma unroll
+        for (int w = 0; w < NWIN / 2; ++w) all = all && (fm[w] == ~0ull);
+        return all;
     }
 
     // a rate-0 subtree: decisions = frozen values, encoding = their polar transform
     static PCUB_HD uint32_t frozen(uint64_t* ub, const uint64_t* fv, int j) {
-        if constexpr (NW == 1) {
-            ub[0] = fv[0] & WMASK;
-            return frozen_local<S, G>(fv[0], j);
+        if constexpr (NWIN == 1) {
+            constexpr uint64_t WM = (L * G == 64) ? ~0ull : ((1ull << (L * G)) - 1ull);
+            ub[0] = fv[0] & WM;
+            return frozen_local<L, G>(fv[0], j);
         } else {
-            constexpr int H = S / 2;
-            ub[0] = fv[0];
-            ub[1] = fv[1];
-            const uint32_t ym = frozen_local<H, G>(fv[0], j), yp = frozen_local<H, G>(fv[1], j);
+            constexpr int H = L / 2;
+            const uint32_t ym = WinTree<H, G, NWIN / 2>::frozen(ub, fv, j);
+            const uint32_t yp = WinTree<H, G, NWIN / 2>::frozen(ub + NWIN / 2, fv + NWIN / 2, j);
             return (ym ^ yp) | (yp << H);
         }
     }
+};
+
+template <int S, int G>
+struct SubWin {
+    static constexpr int SU = S * G;
+    static constexpr int NW = SU > 64 ? SU / 64 : 1;
+    static constexpr int SUW = SU > 64 ? 64 : SU;  // bits per window
+    static constexpr uint64_t WMASK = (SUW == 64) ? ~0ull : ((1ull << SUW) - 1ull);
+    static_assert(SU <= 256, "at most four windows");
+
+    // decisions of the subtree from its S level-D values
+    static PCUB_HD uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm, const uint64_t* fv, int lane) {
+        return WinTree<S, G, NW>::run(v, ub, fm, fv, lane);
+    }
+
+    static PCUB_HD uint32_t frozen(uint64_t* ub, const uint64_t* fv, int j) { return WinTree<S, G, NW>::frozen(ub, fv, j); }
 };
 
 // NT: 0 = cached loads/stores, 1 = non-temporal input rows, 2 = also the upper stage levels

@@ -1,0 +1,103 @@
+"""Monte-Carlo batches and the multi-GPU plumbing around the decoder.
+
+One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on ROCm,
+"gloo" for CPU tests).  Codewords are independent and SC is sequential within a
+codeword, so a Monte-Carlo run shards by codeword: rank r owns its own batch and
+the only collective is one all_reduce of the int64 counters {codewords, frame
+errors, bit errors, symbol errors} plus a max-reduce of the elapsed time.  There is
+no data-path collective because none is needed.
+
+The batch generators below produce synthetic channel outputs on the device
+(torch Philox): random information -> GPU polar encoder -> channel.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+from . import channel, sc
+
+
+def dist_env():
+    """(world_size, rank, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard_seed(seed, rank):
+    """Generator seed of rank r's shard (distinct streams per rank)."""
+    return int(seed) + 7919 * int(rank)
+
+
+def shard_range(total, rank, world):
+    """Rank r's slice [lo, hi) of `total` codewords: contiguous, sizes differ by at most one."""
+    lo = (total * rank) // world
+    hi = (total * (rank + 1)) // world
+    return lo, hi
+
+
+def reduce_counters(counters, elapsed, device=None):
+    """Sum the int64 counters and max the elapsed time over all ranks (no-op when not
+    distributed).  device: where the collective's tensors live (a CUDA device for RCCL,
+    None = CPU for gloo).  Returns (list of ints, float)."""
+    c = torch.tensor([int(v) for v in counters], dtype=torch.int64, device=device)
+    e = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    return [int(v) for v in c.tolist()], float(e.item())
+
+
+def error_counts(decoded, sent):
+    """(frame errors, bit/symbol errors) between [B, K] decoded and sent information."""
+    if decoded.shape[1] == 0:
+        return 0, 0
+    diff = decoded != sent
+    return int(diff.any(dim=1).sum().item()), int(diff.sum().item())
+
+
+def awgn_batch(code, B, sigma2, generator, chunk=1 << 18):
+    """Uniform information -> GPU encoder -> BI-AWGN joint pairs, native [N, B, 2] layout.
+    Returns (xy, info [B, K] uint8)."""
+    dev = code.device
+    xy = torch.empty((code.N, B, 2), dtype=torch.float64, device=dev)
+    info = torch.empty((B, code.K), dtype=torch.uint8, device=dev)
+    for b0 in range(0, B, chunk):
+        b1 = min(B, b0 + chunk)
+        inf = torch.randint(0, 2, (b1 - b0, code.K), dtype=torch.uint8, device=dev, generator=generator)
+        info[b0:b1] = inf
+        xw = sc.encode_native(code, sc.pack(inf))
+        channel.awgn_pairs_native(channel.bits_from_words(xw, code.N), sigma2, generator=generator,
+                                  out=xy[:, b0:b1, :])
+    return xy, info
+
+
+def deletion_batch(code, B, n0, xi, pd, generator, chunk=1 << 17):
+    """Uniform information -> GPU encoder -> guard bands -> deletion channel.
+    Returns (rx [B, W] uint8, rx_len [B] int32, info [B, K] uint8)."""
+    dev = code.device
+    rxs, lens, infos = [], [], []
+    for b0 in range(0, B, chunk):
+        b1 = min(B, b0 + chunk)
+        inf = torch.randint(0, 2, (b1 - b0, code.K), dtype=torch.uint8, device=dev, generator=generator)
+        x = sc.encode(code, inf)
+        rx, ln = channel.deletion_words(x, code.n, n0, xi, pd, generator=generator)
+        rxs.append(rx)
+        lens.append(ln)
+        infos.append(inf)
+    return torch.cat(rxs), torch.cat(lens), torch.cat(infos)
+
+
+def qsc_batch(code, B, p, generator, chunk=1 << 16):
+    """Uniform q-ary information -> GPU q-ary encoder -> QSC(p) joint rows, native [N, B, q].
+    Returns (xy, info [B, K] uint8)."""
+    dev = code.device
+    xy = torch.empty((code.N, B, code.q), dtype=torch.float64, device=dev)
+    info = torch.empty((B, code.K), dtype=torch.uint8, device=dev)
+    for b0 in range(0, B, chunk):
+        b1 = min(B, b0 + chunk)
+        inf = torch.randint(0, code.q, (b1 - b0, code.K), dtype=torch.uint8, device=dev, generator=generator)
+        info[b0:b1] = inf
+        x = sc.encode_qary(code, inf)  # [b, N]
+        xy[:, b0:b1, :] = channel.qsc_pairs_native(x.t(), code.q, p, generator=generator)
+    return xy, info

@@ -7,8 +7,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import bench  # noqa: E402
-from polarcub_amd import construction, sc  # noqa: E402
+from polarcub_amd import construction, mc, sc  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=10)
@@ -23,7 +22,9 @@ fr = construction.bhattacharyya_frozen(a.n, K, s2)
 code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(fr)[0].tolist()), 1)
 sc.set_variant(a.variant)
 dec = sc.BinaryDecoder(code)
-xy, info = bench.make_inputs(code, a.batch, s2, 1, torch.device("cuda"))
+gen = torch.Generator(device="cuda")
+gen.manual_seed(1)
+xy, info = mc.awgn_batch(code, a.batch, s2, gen)
 outs = (torch.empty((code.info_words, a.batch), dtype=torch.int32, device="cuda"),
         torch.empty((code.n_words, a.batch), dtype=torch.int32, device="cuda"), None)
 for _ in range(a.reps):

@@ -104,6 +104,29 @@ int pcub_sc_decode_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B,
                             double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K,
                             uint32_t* info_words, uint32_t* xhat_words, void* stream);
 
+/* Leaf export (LLR check, genie construction).  Decodes like pcub_sc_decode_bin /
+ * pcub_sc_decode_deletion (identical decisions) and also writes, for every u index i,
+ * the normalised xy leaf node the reference passes to calcMarginalizedProbabilities
+ * (BinaryPolarEncoderDecoder.py:250-252, 268-273; the genie's marginalizedUProbs),
+ * as a compact value in leaf[i * B + b]: +r = (1, r), -r = (r, 1), NaN = (0, 0).
+ * No rate-0 subtree is skipped.  frozen_val_cw ([ceil(N/32)][B] words, may be NULL)
+ * gives per-codeword frozen values (the genie's per-trial common randomness,
+ * BinaryPolarEncoderDecoder.py:101-112) and then overrides frozen_val.
+ * info_words / xhat_words may be NULL.  pcub_sc_leaf_bin needs log2N >= 1 and a
+ * workspace of pcub_sc_leaf_bin_workspace(B, log2N) bytes. */
+size_t pcub_sc_leaf_bin_workspace(int64_t B, int32_t log2N);
+int pcub_sc_leaf_bin(const double* xy, int64_t B, int32_t log2N, const uint32_t* frozen_mask, const uint32_t* frozen_val,
+                     const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words, double* leaf,
+                     void* workspace, size_t workspace_bytes, void* stream);
+int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n, int32_t n0,
+                          double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
+                          const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
+                          double* leaf, void* stream);
+/* compact leaves -> the reference's marginals (calcMarginalizedProbabilities,
+ * VectorDistributions/BinaryMemorylessVectorDistribution.py:52-69): s = p0 + p1,
+ * m = p / s, (0.5, 0.5) when s = 0.  count values in, [count][2] f64 out. */
+int pcub_leaf_marginals(const double* leaf, int64_t count, double* marginals, void* stream);
+
 /* [B][nbits] u8 (0/1) -> ceil(nbits/32) x B words, and back. */
 int pcub_pack_bits(const uint8_t* bits, int64_t B, int32_t nbits, uint32_t* words, void* stream);
 int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits, uint8_t* bits, void* stream);

@@ -564,6 +564,57 @@ def fx_deletion_edge(R, timing):
     save("deletion_edge", dict(cases=len(cases), note="(n, n0, pd, ones) per case; words 0-4 adversarial"), **out)
 
 
+def fx_genie_bsc(R, timing):
+    """The reference's genie construction (genieEncodeDecodeSimulation, BinaryPolarEncoderDecoder.py:390-491)
+    on BSC(0.11), n=6, 300 trials, trustXYProbs=True, with a seeded channel RNG; records the
+    TV and Pe vectors it hands to frozenSetFromTVAndPe and the frozen set it returns."""
+    import contextlib
+    import io
+    BMD, BPED = R["BMD"], R["BPED"]
+    N, T, p, gseed, cseed, bound = 64, 300, 0.11, 77, 5, 0.05
+    bsc = BMD.makeBSC(p)
+    crng = random.Random(cseed)
+
+    def make_x():
+        xd = BMD.BinaryMemorylessDistribution()
+        xd.probs.append([bsc.calcXMarginal(0), bsc.calcXMarginal(1)])
+        return xd.makeBinaryMemorylessVectorDistribution(N, None)
+
+    def channel(codeword):  # test2.py:29-50 with an explicit RNG instance
+        out = []
+        for x in codeword:
+            rnd = crng.random()
+            acc = 0.0
+            for y in range(2):
+                if acc + bsc.probXGivenY(int(x), y) >= rnd:
+                    out.append(y)
+                    break
+                acc += bsc.probXGivenY(int(x), y)
+        return out
+
+    def make_xy(received):
+        return bsc.makeBinaryMemorylessVectorDistribution(len(received), received)
+
+    cap = {}
+    orig = BPED.frozenSetFromTVAndPe
+
+    def capture(TV, Pe, b):
+        cap["TV"], cap["Pe"] = [float(v) for v in TV], [float(v) for v in Pe]
+        return orig(TV, Pe, b)
+
+    BPED.frozenSetFromTVAndPe = capture
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            frozen = BPED.genieEncodeDecodeSimulation(N, make_x, lambda e: e, channel, make_xy, T, bound,
+                                                      genieSeed=gseed, trustXYProbs=True)
+    finally:
+        BPED.frozenSetFromTVAndPe = orig
+    save("genie_bsc_n64", dict(N=N, trials=T, p=p, genie_seed=gseed, channel_seed=cseed, bound=bound,
+                               trust=True),
+         TV=np.array(cap["TV"]), Pe=np.array(cap["Pe"]),
+         frozen=np.array([1 if i in frozen else 0 for i in range(N)], np.uint8))
+
+
 FIXTURES = {
     "bsc_n64": fx_bsc_n64,
     "awgn_n1024": lambda R, t: fx_awgn(R, t, 10, 64, 2.0, 20250204, "awgn_n1024", "C2"),
@@ -576,6 +627,7 @@ FIXTURES = {
     "harness_bsc_n64": fx_harness,
     "deletion_n8": fx_deletion,
     "deletion_edge": fx_deletion_edge,
+    "genie_bsc_n64": fx_genie_bsc,
 }
 
 

@@ -69,10 +69,11 @@ def _check_joint(p):
 
 
 def eta(p):
-    """-p log2 p with eta(0) = 0 (ScalarDistributions/BinaryMemorylessDistribution.py)."""
+    """-p log2 p with eta(0) = 0 (ScalarDistributions/BinaryMemorylessDistribution.py:451-459)."""
     import math
-    assert 0 <= p <= 1
-    return 0.0 if p == 0 else -p * math.log2(p)
+    assert 0.0 <= p <= 1.0 + 10 * sys.float_info.epsilon
+    p = min(1.0, p)
+    return 0.0 if p == 0.0 else -p * math.log2(p)
 
 
 class BinaryPolarEncoderDecoder:
@@ -338,33 +339,98 @@ def encodeDecodeSimulation(length, make_xVectorDistribution, make_codeword, simu
     print("Error probability = ", errors, "/", numberOfTrials, " = ", errors / numberOfTrials)
 
 
+def _genie_u(length, seed):
+    """The genie's frozen values for one trial: u_i = 0 if 0.5 >= r_i else 1 with r_i the
+    MT19937 draws of Random(seed) (BinaryPolarEncoderDecoder.py:33-44, 258-262; uniform prior)."""
+    rng = random.Random()
+    rng.seed(seed)
+    return np.array([0 if 0.5 >= rng.random() else 1 for _ in range(length)], np.uint8)
+
+
+def _genie_stats(m, u, trustXYProbs):
+    """Pe / H of one genie decode from its leaf marginals m [N, 2] and the genie's u
+    (genieSingleDecodeSimulatioan, BinaryPolarEncoderDecoder.py:114-178)."""
+    if trustXYProbs:
+        pe = [float(min(a, b)) for a, b in m]
+        h = [eta(float(a)) + eta(float(b)) for a, b in m]
+        return pe, h
+    mu = m[np.arange(len(u)), u]
+    mo = m[np.arange(len(u)), 1 - u]
+    pe = np.where(mu > mo, 0.0, np.where(mu == mo, 0.5, 1.0))
+    return [float(v) for v in pe], []
+
+
 def genieEncodeDecodeSimulation(length, make_xVectorDistribution, make_codeword, simulateChannel,
                                 make_xyVectrorDistribution, numberOfTrials, errorUpperBoundForFrozenSet, genieSeed,
                                 trustXYProbs=True, filename=None):
     """Genie construction run (BinaryPolarEncoderDecoder.py:390-491); returns the frozen set
-    and optionally writes the frozen-set file in the reference's format."""
+    and optionally writes the frozen-set file in the reference's format.
+
+    Batched: the per-trial seeds, common randomness and the user's closures run on the
+    host in trial order (consuming their RNGs exactly as the reference does); under a
+    uniform prior the genie encoder is the GPU polar transform and the genie decodes of
+    memoryless and deletion-collection trials run on the GPU with every leaf exported
+    (pcub_sc_leaf_bin / pcub_sc_leaf_deletion, per-trial frozen values).  Other plugins
+    use the generic per-trial recursion.  Statistics are accumulated in trial order."""
     xvd = make_xVectorDistribution()
     encDec = BinaryPolarEncoderDecoder(length, set(), 0)
     seed_rng = random.Random()
     seed_rng.seed(genieSeed)
+    uniform = _is_uniform_prior(xvd)
     TV = Pe = HEnc = HDec = None
     codeword = []
-    for _ in range(numberOfTrials):
-        s = seed_rng.randint(1, 1000000)
-        (encoded, tv, henc) = encDec.genieSingleEncodeSimulatioan(xvd, s)
-        codeword = make_codeword(encoded)
-        received = simulateChannel(codeword)
-        xyvd = make_xyVectrorDistribution(received)
-        (_, pe, hdec) = encDec.genieSingleDecodeSimulatioan(xvd, xyvd, s, trustXYProbs)
-        if TV is None:
-            TV, Pe, HEnc, HDec = list(tv), list(pe), list(henc), list(hdec)
+    chunk = 1 << 12
+    for t0 in range(0, numberOfTrials, chunk):
+        T = min(chunk, numberOfTrials - t0)
+        seeds = [seed_rng.randint(1, 1000000) for _ in range(T)]
+        enc_stats = []
+        if uniform:
+            U = np.stack([_genie_u(length, s) for s in seeds])
+            enc_all = BinaryPolarEncoderDecoder(length, set(), 0).encode_batch(U)  # K = N: x = polar(u)
+            h_half = eta(0.5) + eta(0.5)
+            for t in range(T):
+                enc_stats.append((enc_all[t], [abs(0.5 - 0.5)] * length, [h_half] * length))
         else:
-            for i in range(len(TV)):
-                TV[i] += tv[i]
-                Pe[i] += pe[i]
-                HEnc[i] += henc[i]
-                if trustXYProbs:
-                    HDec[i] += hdec[i]
+            U = None
+            for s in seeds:
+                enc_stats.append(encDec.genieSingleEncodeSimulatioan(xvd, s))
+        items, bin_rows, del_rows = [], [], {}
+        for t in range(T):
+            codeword = make_codeword(enc_stats[t][0])
+            received = simulateChannel(codeword)
+            xyvd = make_xyVectrorDistribution(received)
+            shape = _deletion_kernel_shape(xyvd) if uniform else None
+            if uniform and _is_memoryless_binary(xyvd) and length >= 2:
+                items.append(("bin", len(bin_rows)))
+                bin_rows.append(_check_joint(xyvd.probs))
+            elif shape is not None:
+                rows = del_rows.setdefault(shape, [])
+                items.append((shape, len(rows)))
+                rows.append((t, xyvd.deletion_source[0]))
+            else:
+                items.append(("host", encDec.genieSingleDecodeSimulatioan(xvd, xyvd, seeds[t], trustXYProbs)))
+        marg = {}
+        if bin_rows:
+            marg["bin"] = _device_genie_bin(length, np.stack(bin_rows), U[[t for t, it in enumerate(items)
+                                                                            if it[0] == "bin"]])
+        for shape, rows in del_rows.items():
+            marg[shape] = _device_genie_deletion(length, shape, [w for _, w in rows], U[[t for t, _ in rows]])
+        for t in range(T):
+            kind, val = items[t]
+            if kind == "host":
+                _, pe, hdec = val
+            else:
+                pe, hdec = _genie_stats(marg[kind][val], U[t], trustXYProbs)
+            _, tv, henc = enc_stats[t]
+            if TV is None:
+                TV, Pe, HEnc, HDec = list(tv), list(pe), list(henc), list(hdec)
+            else:
+                for i in range(len(TV)):
+                    TV[i] += tv[i]
+                    Pe[i] += pe[i]
+                    HEnc[i] += henc[i]
+                    if trustXYProbs:
+                        HDec[i] += hdec[i]
     hes = hds = 0.0
     for i in range(len(TV)):
         TV[i] /= numberOfTrials
@@ -388,6 +454,28 @@ def genieEncodeDecodeSimulation(length, make_xVectorDistribution, make_codeword,
     if filename is not None:
         write_frozen_file(filename, frozenSet, numberOfTrials, TV, Pe)
     return frozenSet
+
+
+def _device_genie_bin(length, xy, U):
+    """Genie decodes of memoryless trials on the GPU: all positions frozen to the trial's u.
+    Returns leaf marginals [T, N, 2] (numpy)."""
+    import torch
+
+    from . import sc
+    code = sc.CodeSpec(length, np.ones(length, np.uint8), np.zeros(length, np.uint8))
+    _, _, m = sc.LeafDecoder(code).decode(torch.from_numpy(xy).to(code.device), torch.from_numpy(U).to(code.device))
+    return m.cpu().numpy()
+
+
+def _device_genie_deletion(length, shape, words, U):
+    import torch
+
+    from . import sc
+    pd, n, n0 = shape
+    code = sc.CodeSpec(length, np.ones(length, np.uint8), np.zeros(length, np.uint8))
+    rx, ln = sc.pad_words(words, code.device)
+    _, _, m = sc.DeletionDecoder(code, n0, pd).decode_leaves(rx, ln, torch.from_numpy(U).to(code.device))
+    return m.cpu().numpy()
 
 
 def write_frozen_file(filename, frozenSet, numberOfTrials, TVvec, Pevec, argv=None):

@@ -44,39 +44,75 @@ struct DelArgs {
     double pd;
     const uint32_t* fmask;
     const uint32_t* fval;
-    uint32_t* info;         // [ceil(K/32)][B]
+    uint32_t* info;         // [ceil(K/32)][B] or null
     uint32_t* xhat;         // [ceil(N/32)][B] or null
+    const uint32_t* fval_cw;  // [ceil(N/32)][B] per-codeword frozen values (export mode), or null
+    double* leaf;           // [N][B] compact normalised leaves (export mode)
+};
+
+// XSub (sc_bin_body.h) for the export mode: no rate-0 node is skipped and the two
+// normalised leaves of every M = 2 node are written (by group position 0) at
+// leaf[u * B] -- the xy marginals the genie reads (BinaryPolarEncoderDecoder.py:268-273).
+template <int M, int UBASE>
+struct XSubE {
+    __device__ static uint32_t run(double v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane, double* leaf,
+                                   long long B, bool store) {
+        const double w = xor_shfl(v, M / 2);
+        const bool lo = (lane & (M / 2)) == 0;
+        const double a = lo ? v : w, b = lo ? w : v;
+        if constexpr (M == 2) {
+            const double c0 = op_f(a, b);
+            const uint32_t u0 = ((fm >> UBASE) & 1u) ? (uint32_t)((fv >> UBASE) & 1u) : leaf_v(c0);
+            const double c1 = op_g(a, b, u0);
+            const uint32_t u1 = ((fm >> (UBASE + 1)) & 1u) ? (uint32_t)((fv >> (UBASE + 1)) & 1u) : leaf_v(c1);
+            if (store) {
+                leaf[(long long)UBASE * B] = c0;
+                leaf[(long long)(UBASE + 1) * B] = c1;
+            }
+            ub |= ((uint64_t)u0 << UBASE) | ((uint64_t)u1 << (UBASE + 1));
+            return lo ? (u0 ^ u1) : u1;
+        } else {
+            constexpr int H = M / 2;
+            const uint32_t ym = XSubE<H, UBASE>::run(op_f(a, b), ub, fm, fv, lane, leaf, B, store);
+            const uint32_t yp = XSubE<H, UBASE + H>::run(op_g(a, b, ym), ub, fm, fv, lane, leaf, B, store);
+            return lo ? (ym ^ yp) : yp;
+        }
+    }
 };
 
 // Per-lane decoding context: frozen windows, decisions, information accumulator.
-template <int T>
+template <int T, bool EXP>
 struct DelCtx {
     const DelArgs* A;
     long long cw;
-    bool leader;  // group position 0 stores the information words
+    bool leader;  // group position 0 stores the information words and exported leaves
     int lane;
     int k;        // next memoryless subtree (u range [k*T, (k+1)*T))
     uint32_t acc;
     int nacc;
     int infow;
 
-    PCUB_HD uint64_t window(const uint32_t* w) const {
+    // bits [k*T, (k+1)*T) of a bit vector whose word i is w[i * stride]
+    PCUB_HD uint64_t window(const uint32_t* w, long long stride = 1) const {
         const int us = k * T;
         if constexpr (T == 64) {
-            return (uint64_t)w[us >> 5] | ((uint64_t)w[(us >> 5) + 1] << 32);
+            return (uint64_t)w[(us >> 5) * stride] | ((uint64_t)w[((us >> 5) + 1) * stride] << 32);
         } else {
-            return (uint64_t)((w[us >> 5] >> (us & 31)) & (uint32_t)((1ull << T) - 1ull));
+            return (uint64_t)((w[(us >> 5) * stride] >> (us & 31)) & (uint32_t)((1ull << T) - 1ull));
         }
     }
 
     // SC over the collapsed memoryless node (one compact value per lane); returns
     // this lane's bit of the node's re-encoded vector (natural position = its trellis).
     __device__ uint32_t subtree(double v) {
-        const uint64_t fm = window(A->fmask), fv = window(A->fval);
+        const uint64_t fm = window(A->fmask);
+        const uint64_t fv = A->fval_cw ? window(A->fval_cw + cw, A->B) : window(A->fval);
         uint64_t ub = 0;
         uint32_t y;
         constexpr uint64_t WM = (T == 64) ? ~0ull : ((1ull << T) - 1ull);
-        if (fm == WM) {  // rate-0 node: decisions are the frozen values
+        if constexpr (EXP) {
+            y = XSubE<T, 0>::run(v, ub, fm, fv, lane, A->leaf + (long long)k * T * A->B + cw, A->B, leader) & 1u;
+        } else if (fm == WM) {  // rate-0 node: decisions are the frozen values
             ub = fv;
             y = frozen_local<1, T>(fv, lane & (T - 1));
         } else {
@@ -85,7 +121,7 @@ struct DelCtx {
         for (uint64_t im = ~fm & WM; im != 0ull; im &= im - 1ull) {
             acc |= (uint32_t)((ub >> __builtin_ctzll(im)) & 1ull) << nacc;
             if (++nacc == 32) {
-                if (leader) A->info[(long long)infow * A->B + cw] = acc;
+                if (leader && A->info) A->info[(long long)infow * A->B + cw] = acc;
                 acc = 0;
                 nacc = 0;
                 ++infow;
@@ -105,10 +141,10 @@ struct DelCap {
 
 // One SC node of the trellis levels: trellis `t` of length LEN (this lane's
 // slice of the collection).  Returns the node's re-encoded slice, natural order.
-template <int L, int T, int LEN>
+template <int L, int T, int LEN, bool EXP>
 struct DelNode {
     template <class PT>
-    __device__ static uint32_t run(const PT& t, DelCtx<T>& cx) {
+    __device__ static uint32_t run(const PT& t, DelCtx<T, EXP>& cx) {
         using Cap = DelCap<L>;
         if constexpr (LEN == 2) {
             // children are length-1 trellises collapsed to memoryless rows
@@ -127,10 +163,10 @@ struct DelNode {
             Trel<H, Cap::V, Cap::E1> c;
             trellis_transform<LEN>(t, c, nullptr);
             trellis_normalize<H>(c);
-            const uint32_t ym = DelNode<L, T, H>::run(c, cx);
+            const uint32_t ym = DelNode<L, T, H, EXP>::run(c, cx);
             trellis_transform<LEN>(t, c, &ym);
             trellis_normalize<H>(c);
-            const uint32_t yp = DelNode<L, T, H>::run(c, cx);
+            const uint32_t yp = DelNode<L, T, H, EXP>::run(c, cx);
             uint32_t x = 0;  // x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h]
 #pragma unroll
             for (int h = 0; h < H; ++h)
@@ -140,7 +176,7 @@ struct DelNode {
     }
 };
 
-template <int N0, int TB>
+template <int N0, int TB, bool EXP>
 __global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
     constexpr int L = 1 << N0;
     constexpr int T = 1 << TB;
@@ -169,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
     Trel<L, Cap::V, Cap::E0> base;
     trellis_build<L>(base, bit, s, m, A.pd);
 
-    DelCtx<T> cx;
+    DelCtx<T, EXP> cx;
     cx.A = &A;
     cx.cw = cw;
     cx.leader = valid && p == 0;
@@ -178,8 +214,8 @@ __global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
     cx.acc = 0;
     cx.nacc = 0;
     cx.infow = 0;
-    const uint32_t x = DelNode<L, T, L>::run(base, cx);
-    if (cx.nacc && cx.leader) A.info[(long long)cx.infow * A.B + cw] = cx.acc;
+    const uint32_t x = DelNode<L, T, L, EXP>::run(base, cx);
+    if (cx.nacc && cx.leader && A.info) A.info[(long long)cx.infow * A.B + cw] = cx.acc;
 
     // x_hat: trellis t's slice is natural positions [t*L, (t+1)*L)
     __syncthreads();
@@ -192,38 +228,43 @@ __global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
 
 typedef void (*DelKern)(DelArgs);
 
-template <int N0>
+template <int N0, bool EXP>
 DelKern del_kernel_tb(int tb) {
     switch (tb) {
-        case 1: return k_sc_del<N0, 1>;
-        case 2: return k_sc_del<N0, 2>;
-        case 3: return k_sc_del<N0, 3>;
-        case 4: return k_sc_del<N0, 4>;
-        case 5: return k_sc_del<N0, 5>;
-        case 6: return k_sc_del<N0, 6>;
+        case 1: return k_sc_del<N0, 1, EXP>;
+        case 2: return k_sc_del<N0, 2, EXP>;
+        case 3: return k_sc_del<N0, 3, EXP>;
+        case 4: return k_sc_del<N0, 4, EXP>;
+        case 5: return k_sc_del<N0, 5, EXP>;
+        case 6: return k_sc_del<N0, 6, EXP>;
         default: return nullptr;
     }
 }
 
+template <bool EXP>
 DelKern del_kernel(int n0, int tb) {
     switch (n0) {
-        case 1: return del_kernel_tb<1>(tb);
-        case 2: return del_kernel_tb<2>(tb);
-        case 3: return del_kernel_tb<3>(tb);
+        case 1: return del_kernel_tb<1, EXP>(tb);
+        case 2: return del_kernel_tb<2, EXP>(tb);
+        case 3: return del_kernel_tb<3, EXP>(tb);
         default: return nullptr;
     }
 }
 
 }  // namespace
 
-extern "C" int pcub_sc_deletion_supported(int32_t n, int32_t n0) { return del_kernel(n0, n - n0) != nullptr; }
+extern "C" int pcub_sc_deletion_supported(int32_t n, int32_t n0) { return del_kernel<false>(n0, n - n0) != nullptr; }
 
-extern "C" int pcub_sc_decode_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n,
-                                       int32_t n0, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
-                                       int32_t K, uint32_t* info_words, uint32_t* xhat_words, void* stream) {
-    const DelKern kern = del_kernel(n0, n - n0);
-    if (!kern || B < 0 || stride < 0 || stride > 32767 || !frozen_mask || !frozen_val) return PCUB_EINVAL;
-    if (K < 0 || K > (1 << n) || (K > 0 && !info_words) || (B > 0 && (!rx || !rx_len))) return PCUB_EINVAL;
+namespace {
+
+int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n, int32_t n0,
+               double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val, const uint32_t* frozen_val_cw,
+               int32_t K, uint32_t* info_words, uint32_t* xhat_words, double* leaf, void* stream) {
+    const DelKern kern = exp ? del_kernel<true>(n0, n - n0) : del_kernel<false>(n0, n - n0);
+    if (!kern || B < 0 || stride < 0 || stride > 32767 || !frozen_mask || (!frozen_val && !frozen_val_cw))
+        return PCUB_EINVAL;
+    if (K < 0 || K > (1 << n) || (!exp && K > 0 && !info_words) || (B > 0 && (!rx || !rx_len))) return PCUB_EINVAL;
+    if (exp && !leaf) return PCUB_EINVAL;
     if (!(pd >= 0.0 && pd <= 1.0)) return PCUB_EINVAL;
     if (B == 0) return 0;
     DelArgs A;
@@ -235,10 +276,30 @@ extern "C" int pcub_sc_decode_deletion(const uint8_t* rx, const int32_t* rx_len,
     A.pd = pd;
     A.fmask = frozen_mask;
     A.fval = frozen_val;
+    A.fval_cw = frozen_val_cw;
     A.info = info_words;
     A.xhat = xhat_words;
+    A.leaf = leaf;
     const long long cpb = kBlock >> (n - n0);
     const long long grid = (B + cpb - 1) / cpb;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, A);
     return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int pcub_sc_decode_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n,
+                                       int32_t n0, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
+                                       int32_t K, uint32_t* info_words, uint32_t* xhat_words, void* stream) {
+    if (!frozen_val) return PCUB_EINVAL;
+    return launch_del(false, rx, rx_len, B, stride, n, n0, pd, frozen_mask, frozen_val, nullptr, K, info_words,
+                      xhat_words, nullptr, stream);
+}
+
+extern "C" int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n,
+                                     int32_t n0, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
+                                     const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words,
+                                     uint32_t* xhat_words, double* leaf, void* stream) {
+    return launch_del(true, rx, rx_len, B, stride, n, n0, pd, frozen_mask, frozen_val, frozen_val_cw, K, info_words,
+                      xhat_words, leaf, stream);
 }

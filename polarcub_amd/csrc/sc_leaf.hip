@@ -1,0 +1,215 @@
+// sc_leaf.hip -- binary SC decode that also exports every leaf's distribution
+// (LLR check, genie construction), gfx950, + C-ABI launchers.
+//
+// pcub_sc_leaf_bin decodes exactly like pcub_sc_decode_bin (same decisions,
+// BinaryPolarEncoderDecoder.py:223-325) and additionally writes, for every u
+// index i, the normalised xy leaf the reference hands to
+// calcMarginalizedProbabilities (VectorDistributions/BinaryMemorylessVectorDistribution.py:52-69)
+// -- what recursiveEncodeDecode collects into marginalizedUProbs (:268-273) and
+// what the genie turns into Pe / H (genieSingleDecodeSimulatioan, :114-178).
+// Frozen values may be given per codeword (the genie draws a fresh common
+// randomness for every trial, :101-112), and no rate-0 subtree is skipped:
+// every leaf is evaluated.
+//
+// This is the simple schedule (one codeword per lane, every stage level in a
+// per-slot scratch, half-split node order as in sc_bin_body.h); it is the
+// export path, not the throughput path.
+#include <hip/hip_runtime.h>
+
+#include "polarcub_sc.h"
+#include "sc_common.h"
+
+using namespace pcub;
+
+namespace {
+
+constexpr int kLBlock = 256;
+
+struct LeafArgs {
+    const double2* xy;          // [N][B] raw pairs
+    long long B;
+    int n;
+    const uint32_t* fmask;      // ceil(N/32)
+    const uint32_t* fval;       // ceil(N/32), or null when fval_cw is given
+    const uint32_t* fval_cw;    // [ceil(N/32)][B] per-codeword frozen values, or null
+    uint32_t* info;             // [ceil(K/32)][B] or null
+    uint32_t* xhat;             // [ceil(N/32)][B] or null
+    double* leaf;               // [N][B] compact normalised leaf values
+    double* scratch;            // [N - 2][nslots]
+    uint8_t* ybits;             // [N][nslots]
+    long long nslots;
+};
+
+PCUB_HD uint32_t word_bit(const uint32_t* w, int i) { return (w[i >> 5] >> (i & 31)) & 1u; }
+
+__device__ void leaf_cw(const LeafArgs& A, long long cw, long long slot, bool store) {
+    const int n = A.n;
+    const int N = 1 << n;
+    const long long B = A.B, ns = A.nslots;
+    double* scr = A.scratch + slot;
+    uint8_t* Y = A.ybits + slot;
+    auto fbit = [&](int i) -> uint32_t {
+        return A.fval_cw ? ((A.fval_cw[(long long)(i >> 5) * B + cw] >> (i & 31)) & 1u) : word_bit(A.fval, i);
+    };
+    uint32_t acc = 0;
+    int nacc = 0, infow = 0;
+    auto put_info = [&](uint32_t u) {
+        acc |= u << nacc;
+        if (++nacc == 32) {
+            if (store && A.info) A.info[(long long)(infow)*B + cw] = acc;
+            ++infow;
+            acc = 0;
+            nacc = 0;
+        }
+    };
+    const int D = n - 1;  // depth of the 2-value nodes
+    for (int k = 0; k < (1 << D); ++k) {
+        const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
+        double v0 = 0.0, v1 = 0.0;
+        bool raw = false;  // N = 2: the 2-value node is the (never normalised) root
+        double2 r0, r1;
+        if (D == 0) {
+            raw = true;
+            r0 = A.xy[cw];
+            r1 = A.xy[B + cw];
+        }
+        for (int d = d0; d <= D; ++d) {
+            const bool gop = (d == d0) && (k != 0);
+            const int Lo = N >> d;
+            const int ystart = (k >> (D - d + 1)) * (N >> (d - 1));
+            for (int p = 0; p < Lo; ++p) {
+                const uint32_t u = gop ? Y[(long long)(ystart + p) * ns] : 0u;
+                double o;
+                if (d == 1) {
+                    const long long q = (long long)bitrev((uint32_t)p, n - 1);
+                    const double2 a = A.xy[(2 * q) * B + cw], b = A.xy[(2 * q + 1) * B + cw];
+                    o = gop ? op_g_raw(a, b, u) : op_f_raw(a, b);
+                } else {
+                    const long long off = (long long)N - 2 * (N >> (d - 1));
+                    const double a = scr[(off + p) * ns], b = scr[(off + p + Lo) * ns];
+                    o = gop ? op_g(a, b, u) : op_f(a, b);
+                }
+                if (d == D) {
+                    if (p == 0) v0 = o;
+                    else v1 = o;
+                } else {
+                    scr[((long long)N - 2 * Lo + p) * ns] = o;
+                }
+            }
+        }
+        // the two leaves of this depth-D node: normalised minus / plus children
+        const int i0 = 2 * k, i1 = 2 * k + 1;
+        const double c0 = raw ? op_f_raw(r0, r1) : op_f(v0, v1);
+        const uint32_t u0 = word_bit(A.fmask, i0) ? fbit(i0) : leaf_v(c0);
+        const double c1 = raw ? op_g_raw(r0, r1, u0) : op_g(v0, v1, u0);
+        const uint32_t u1 = word_bit(A.fmask, i1) ? fbit(i1) : leaf_v(c1);
+        if (store) {
+            A.leaf[(long long)i0 * B + cw] = c0;
+            A.leaf[(long long)i1 * B + cw] = c1;
+        }
+        if (!word_bit(A.fmask, i0)) put_info(u0);
+        if (!word_bit(A.fmask, i1)) put_info(u1);
+        Y[(long long)i0 * ns] = (uint8_t)(u0 ^ u1);
+        Y[(long long)i1 * ns] = (uint8_t)u1;
+        for (int d = D; d >= 1 && ((k >> (D - d)) & 1); --d) {
+            const int Lc = N >> d;
+            const long long st = (long long)(k >> (D - d + 1)) * 2 * Lc;
+            for (int p = 0; p < Lc; ++p) Y[(st + p) * ns] ^= Y[(st + Lc + p) * ns];
+        }
+    }
+    if (store && nacc && A.info) A.info[(long long)infow * B + cw] = acc;
+    if (store && A.xhat) {
+        for (int w = 0; w < (N + 31) / 32; ++w) {
+            uint32_t o = 0;
+            for (int t = 0; t < 32 && 32 * w + t < N; ++t)
+                o |= (uint32_t)Y[(long long)bitrev((uint32_t)(32 * w + t), n) * ns] << t;
+            A.xhat[(long long)w * B + cw] = o;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kLBlock) void k_sc_leaf(LeafArgs A) {
+    const long long slot = (long long)blockIdx.x * kLBlock + threadIdx.x;
+    const long long ntiles = (A.B + kLBlock - 1) / kLBlock;
+    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const long long cw = t * kLBlock + threadIdx.x;
+        const bool valid = cw < A.B;
+        leaf_cw(A, valid ? cw : A.B - 1, slot, valid);
+    }
+}
+
+// compact leaf -> the reference's marginal: s = 0 + p0 + p1; m = p / s, or (0.5, 0.5)
+__global__ __launch_bounds__(kLBlock) void k_leaf_marginals(const double* leaf, long long count, double* m) {
+    const long long i = (long long)blockIdx.x * kLBlock + threadIdx.x;
+    if (i >= count) return;
+    const CV c = cv_load(leaf[i]);
+    double p0 = c.s ? c.r : 1.0, p1 = c.s ? 1.0 : c.r;
+    if (c.r != c.r) p0 = p1 = 0.0;  // the (0, 0) sentinel
+    double s = 0.0;
+    s += p0;
+    s += p1;
+    m[2 * i] = s > 0.0 ? p0 / s : 0.5;
+    m[2 * i + 1] = s > 0.0 ? p1 / s : 0.5;
+}
+
+long long leaf_grid(long long B) {
+    int dev = 0, cus = 0, occ = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sc_leaf, kLBlock, 0) != hipSuccess || occ < 1) occ = 1;
+    const long long ntiles = (B + kLBlock - 1) / kLBlock;
+    const long long g = (long long)cus * occ;
+    return ntiles < g ? ntiles : g;
+}
+
+size_t leaf_slot_bytes(int n) {
+    const size_t N = (size_t)1 << n;
+    return (N > 2 ? N - 2 : 1) * sizeof(double) + N;
+}
+
+}  // namespace
+
+extern "C" size_t pcub_sc_leaf_bin_workspace(int64_t B, int32_t log2N) {
+    if (B <= 0 || log2N < 1 || log2N > 20) return 0;
+    return (size_t)leaf_grid(B) * kLBlock * leaf_slot_bytes(log2N);
+}
+
+extern "C" int pcub_sc_leaf_bin(const double* xy, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                                const uint32_t* frozen_val, const uint32_t* frozen_val_cw, int32_t K,
+                                uint32_t* info_words, uint32_t* xhat_words, double* leaf, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+    if (B < 0 || log2N < 1 || log2N > 20 || !frozen_mask || (!frozen_val && !frozen_val_cw) || !leaf)
+        return PCUB_EINVAL;
+    if (K < 0 || K > (1 << log2N) || (B > 0 && !xy)) return PCUB_EINVAL;
+    if (B == 0) return 0;
+    long long g = leaf_grid(B);
+    if (g <= 0) return (int)hipErrorNoDevice;
+    const size_t per_block = (size_t)kLBlock * leaf_slot_bytes(log2N);
+    if (!workspace) return PCUB_EINVAL;
+    if ((size_t)g * per_block > workspace_bytes) g = (long long)(workspace_bytes / per_block);
+    if (g <= 0) return PCUB_EINVAL;
+    LeafArgs A;
+    A.xy = (const double2*)xy;
+    A.B = B;
+    A.n = log2N;
+    A.fmask = frozen_mask;
+    A.fval = frozen_val;
+    A.fval_cw = frozen_val_cw;
+    A.info = info_words;
+    A.xhat = xhat_words;
+    A.leaf = leaf;
+    A.nslots = g * kLBlock;
+    const size_t N = (size_t)1 << log2N;
+    A.scratch = (double*)workspace;
+    A.ybits = (uint8_t*)workspace + (size_t)A.nslots * (N > 2 ? N - 2 : 1) * sizeof(double);
+    hipLaunchKernelGGL(k_sc_leaf, dim3((unsigned)g), dim3(kLBlock), 0, (hipStream_t)stream, A);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcub_leaf_marginals(const double* leaf, int64_t count, double* marginals, void* stream) {
+    if (count < 0 || (count > 0 && (!leaf || !marginals))) return PCUB_EINVAL;
+    if (count == 0) return 0;
+    hipLaunchKernelGGL(k_leaf_marginals, dim3((unsigned)((count + kLBlock - 1) / kLBlock)), dim3(kLBlock), 0,
+                       (hipStream_t)stream, leaf, (long long)count, marginals);
+    return (int)hipGetLastError();
+}

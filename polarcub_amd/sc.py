@@ -180,6 +180,51 @@ class BinaryDecoder:
         return unpack(info_w, self.code.K), unpack(xh_w, self.code.N)
 
 
+class LeafDecoder:
+    """Binary SC with every leaf exported (pcub_sc_leaf_bin): the xy marginals the reference
+    collects in marginalizedUProbs (LLR checks, genie runs).  Optional per-codeword frozen
+    values ([B, N] 0/1) override the code's."""
+
+    def __init__(self, code):
+        self.code = code
+        self._ws = None
+
+    def decode_native(self, xy, fval_cw=None):
+        """xy [N, B, 2] float64 (device) -> (info_words, xhat_words, leaf [N, B] compact float64)."""
+        c = self.code
+        if xy.dtype != torch.float64 or xy.dim() != 3 or xy.shape[0] != c.N or xy.shape[2] != 2 or not xy.is_cuda:
+            raise ValueError("xy must be a float64 [N, B, 2] device tensor with N=%d" % c.N)
+        if c.n < 1:
+            raise ValueError("leaf export needs N >= 2")
+        xy = xy.contiguous()
+        B = xy.shape[1]
+        need = int(_lib.lib().pcub_sc_leaf_bin_workspace(B, c.n))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 16), dtype=torch.uint8, device=xy.device)
+        fw = None if fval_cw is None else pack(fval_cw.to(device=xy.device, dtype=torch.uint8))
+        info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=xy.device)
+        xh = torch.empty((c.n_words, B), dtype=torch.int32, device=xy.device)
+        leaf = torch.empty((c.N, B), dtype=torch.float64, device=xy.device)
+        rc = _lib.lib().pcub_sc_leaf_bin(_p(xy), B, c.n, _p(c.fmask_dev), _p(c.fval_dev), _p(fw), c.K, _p(info),
+                                         _p(xh), _p(leaf), _p(self._ws), self._ws.numel(), _stream())
+        _lib.check(rc, "pcub_sc_leaf_bin")
+        return info, xh, leaf
+
+    def decode(self, xy, fval_cw=None):
+        """xy [B, N, 2] -> (info [B, K] uint8, xhat [B, N] uint8, marginals [B, N, 2] float64)."""
+        info, xh, leaf = self.decode_native(transpose_pairs(xy), fval_cw)
+        return unpack(info, self.code.K), unpack(xh, self.code.N), leaf_marginals(leaf)
+
+
+def leaf_marginals(leaf):
+    """Compact leaves [N, B] -> the reference's leaf marginals [B, N, 2] (pcub_leaf_marginals)."""
+    N, B = leaf.shape
+    t = leaf.t().contiguous()
+    m = torch.empty((B, N, 2), dtype=torch.float64, device=leaf.device)
+    _lib.check(_lib.lib().pcub_leaf_marginals(_p(t), t.numel(), _p(m), _stream()), "pcub_leaf_marginals")
+    return m
+
+
 def transpose_pairs(xy):
     """[B, N, q] float64 -> [N, B, q] float64 on device."""
     if xy.dtype != torch.float64 or xy.dim() != 3:
@@ -338,6 +383,21 @@ class DeletionDecoder:
         """Returns (info [B, K] uint8, xhat [B, N] uint8) on device."""
         info_w, xh_w = self.decode_native(rx, rx_len)
         return unpack(info_w, self.code.K), unpack(xh_w, self.code.N)
+
+    def decode_leaves(self, rx, rx_len, fval_cw=None):
+        """Export mode (pcub_sc_leaf_deletion): (info [B, K], xhat [B, N], marginals [B, N, 2])."""
+        c = self.code
+        rx = rx.contiguous()
+        B, W = rx.shape
+        ln = rx_len.to(device=rx.device, dtype=torch.int32).contiguous()
+        fw = None if fval_cw is None else pack(fval_cw.to(device=rx.device, dtype=torch.uint8))
+        info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=rx.device)
+        xh = torch.empty((c.n_words, B), dtype=torch.int32, device=rx.device)
+        leaf = torch.empty((c.N, B), dtype=torch.float64, device=rx.device)
+        rc = _lib.lib().pcub_sc_leaf_deletion(_p(rx), _p(ln), B, W, c.n, self.n0, self.pd, _p(c.fmask_dev),
+                                              _p(c.fval_dev), _p(fw), c.K, _p(info), _p(xh), _p(leaf), _stream())
+        _lib.check(rc, "pcub_sc_leaf_deletion")
+        return unpack(info, c.K), unpack(xh, c.N), leaf_marginals(leaf)
 
 
 def pad_words(words, device=None):

@@ -1,0 +1,88 @@
+"""Genie construction (genieEncodeDecodeSimulation) with the GPU leaf-export decoders,
+against the reference's own genie runs: the TV / Pe vectors it derives the frozen set
+from, and the frozen set, bit-exact (memoryless BSC with trusted probabilities; the
+deletion channel of main_deletion.py with trustXYProbs=False)."""
+import contextlib
+import io
+import random
+
+import numpy as np
+import pytest
+
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_capturing(fn):
+    from polarcub_amd import coding
+    cap = {}
+    orig = coding.frozenSetFromTVAndPe
+
+    def capture(TV, Pe, b):
+        cap["TV"], cap["Pe"] = np.array(TV, np.float64), np.array(Pe, np.float64)
+        return orig(TV, Pe, b)
+
+    coding.frozenSetFromTVAndPe = capture
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            frozen = fn()
+    finally:
+        coding.frozenSetFromTVAndPe = orig
+    return frozen, cap
+
+
+def test_genie_bsc_matches_reference():
+    from polarcub_amd import coding, scalar
+    g = load_golden("genie_bsc_n64")
+    m = g["meta"]
+    N = m["N"]
+    bsc = scalar.makeBSC(m["p"])
+    crng = random.Random(m["channel_seed"])
+
+    def make_x():
+        xd = scalar.BinaryMemorylessDistribution()
+        xd.append([bsc.calcXMarginal(0), bsc.calcXMarginal(1)])
+        return xd.makeBinaryMemorylessVectorDistribution(N, None)
+
+    def channel(codeword):
+        out = []
+        for x in codeword:
+            rnd = crng.random()
+            acc = 0.0
+            for y in range(2):
+                if acc + bsc.probXGivenY(int(x), y) >= rnd:
+                    out.append(y)
+                    break
+                acc += bsc.probXGivenY(int(x), y)
+        return out
+
+    frozen, cap = _run_capturing(lambda: coding.genieEncodeDecodeSimulation(
+        N, make_x, lambda e: e, channel, lambda r: bsc.makeBinaryMemorylessVectorDistribution(len(r), r),
+        m["trials"], m["bound"], m["genie_seed"], trustXYProbs=True))
+    assert np.array_equal(cap["TV"], g["TV"])
+    assert np.array_equal(cap["Pe"], g["Pe"])
+    assert np.array_equal(np.array([1 if i in frozen else 0 for i in range(N)], np.uint8), g["frozen"])
+
+
+def test_genie_deletion_matches_reference():
+    from polarcub_amd import coding, deletion, vectors
+    g = load_golden("deletion_n8")
+    m = g["meta"]
+    n, n0, pd, xi = m["n"], m["n0"], m["pd"], m["xi"]
+    N = 1 << n
+    crng = random.Random()
+    crng.seed(m["channel_seed"])
+
+    def make_x():
+        v = vectors.BinaryMemorylessVectorDistribution(N)
+        v.probs[:] = 0.5
+        return v
+
+    frozen, cap = _run_capturing(lambda: coding.genieEncodeDecodeSimulation(
+        N, make_x, lambda e: deletion.addDeletionGuardBands(e, n, n0, xi, 0),
+        lambda c: deletion.deletionChannelSimulation(c, pd, None, crng),
+        lambda r: deletion.buildCollectionOfBinaryTrellises_uniformInput_deletion(r, pd, xi, n, n0, 0),
+        m["genie_trials"], 0.1, m["genie_seed"], trustXYProbs=False))
+    assert np.array_equal(cap["TV"] + cap["Pe"], g["genie_score"])
+    assert np.array_equal(np.array([1 if i in frozen else 0 for i in range(N)], np.uint8), g["genie_frozen"])

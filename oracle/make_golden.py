@@ -615,6 +615,27 @@ def fx_genie_bsc(R, timing):
          frozen=np.array([1 if i in frozen else 0 for i in range(N)], np.uint8))
 
 
+def fx_main_deletion(R, timing):
+    """The reference's main_deletion.py itself (runpy, its own argv parsing) with
+    -n 8 -g 100 -e 40 and default seeds; records its stdout lines."""
+    import contextlib
+    import io
+    import runpy
+    argv = ["main_deletion.py", "-n", "8", "-g", "100", "-e", "40"]
+    old = sys.argv
+    sys.argv = argv
+    buf = io.StringIO()
+    try:
+        with contextlib.redirect_stdout(buf):
+            runpy.run_path(os.path.join(REF, "main_deletion.py"), run_name="__main__")
+    finally:
+        sys.argv = old
+    lines = buf.getvalue().strip().splitlines()
+    keep = [l for l in lines if not l.startswith(("TVVec", "pevec", "HEncvec", "HDecvec"))]
+    print("  reference main_deletion:", keep[-1])
+    save("main_deletion_n8", dict(argv=argv[1:], lines=keep))
+
+
 FIXTURES = {
     "bsc_n64": fx_bsc_n64,
     "awgn_n1024": lambda R, t: fx_awgn(R, t, 10, 64, 2.0, 20250204, "awgn_n1024", "C2"),
@@ -628,6 +649,7 @@ FIXTURES = {
     "deletion_n8": fx_deletion,
     "deletion_edge": fx_deletion_edge,
     "genie_bsc_n64": fx_genie_bsc,
+    "main_deletion_n8": fx_main_deletion,
 }
 
 

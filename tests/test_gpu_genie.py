@@ -86,3 +86,16 @@ def test_genie_deletion_matches_reference():
         m["genie_trials"], 0.1, m["genie_seed"], trustXYProbs=False))
     assert np.array_equal(cap["TV"] + cap["Pe"], g["genie_score"])
     assert np.array_equal(np.array([1 if i in frozen else 0 for i in range(N)], np.uint8), g["genie_frozen"])
+
+
+def test_main_deletion_cli_matches_reference_run():
+    """polarcub_amd.cli.main_deletion with the reference run's argv prints the same lines
+    (the genie vectors aside, whose element repr differs between numpy scalars and floats)."""
+    from polarcub_amd.cli import main_deletion
+    g = load_golden("main_deletion_n8")
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        main_deletion.main(list(g["meta"]["argv"]))
+    lines = [l for l in buf.getvalue().strip().splitlines()
+             if not l.startswith(("TVVec", "pevec", "HEncvec", "HDecvec"))]
+    assert lines == g["meta"]["lines"]

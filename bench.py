@@ -80,9 +80,9 @@ class Awgn:
         self.variant = sc.default_variant() if a.variant is None else a.variant
         sc.set_max_blocks_per_cu(a.max_blocks)
         self.dec = sc.BinaryDecoder(self.code)
-        gen = torch.Generator(device=device)
-        gen.manual_seed(mc.shard_seed(a.seed, rank))
-        self.xy, self.info_tx = mc.awgn_batch(self.code, self.B, self.sigma2, gen)
+        # global codewords [rank*B, (rank+1)*B), Philox keyed by (seed, codeword index)
+        self.info_w, self.xy = mc.philox_batch(self.code, a.seed, rank * self.B, self.B, mc.CHANNEL_AWGN, self.sigma2)
+        self.rank = rank
         self.outs = (torch.empty((self.code.info_words, self.B), dtype=torch.int32, device=device),
                      None if a.no_xhat else torch.empty((self.code.n_words, self.B), dtype=torch.int32, device=device),
                      None)
@@ -93,7 +93,16 @@ class Awgn:
 
     def errors(self):
         d = sc.unpack(self.outs[0], self.K)
-        return mc.error_counts(d, self.info_tx)
+        return mc.error_counts(d, sc.unpack(self.info_w, self.K))
+
+    def end_to_end(self):
+        """The whole Monte-Carlo pipeline on the device (pcub_mc_run_bin: information bits ->
+        encoder -> BI-AWGN -> decode -> counters) over this rank's codewords: seconds."""
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        mc.run_bin(self.code, self.a.seed, self.rank * self.B, self.B, mc.CHANNEL_AWGN, self.sigma2)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
 
     def bytes_alg(self):
         return 16 * self.N + self.N // 8 + self.K // 8  # f64 pairs in + packed x_hat + packed info
@@ -106,8 +115,8 @@ class Awgn:
         return dict(
             metric="decoded codewords/sec at N=%d BI-AWGN, batch=%d per GPU; FER match vs reference" % (self.N, self.B),
             dtype="f64",
-            data="synthetic: uniform info bits, GPU polar encoder, BI-AWGN Eb/N0=%.1f dB pairs generated on device"
-                 % a.ebn0,
+            data="synthetic: uniform info bits, GPU polar encoder, BI-AWGN Eb/N0=%.1f dB pairs generated on device "
+                 "(Philox keyed by global codeword index)" % a.ebn0,
             config={"workload": "binary SC decode N=%d K=%d BI-AWGN %.1f dB (BASELINE configs[%d])"
                                 % (self.N, self.K, a.ebn0, 1 if self.n == 10 else 2),
                     "N": self.N, "K": self.K, "batch_per_gpu": self.B, "ebn0_db": a.ebn0,
@@ -334,6 +343,12 @@ def main():
     counters, elapsed = mc.reduce_counters([w.B, fe, be, 0], elapsed, device if world > 1 else None)
     total_cw = counters[0] * a.steps
     value = total_cw / elapsed
+    e2e = None
+    if hasattr(w, "end_to_end"):
+        if world > 1:
+            dist.barrier()
+        _, e2e_s = mc.reduce_counters([0], w.end_to_end(), device if world > 1 else None)
+        e2e = counters[0] / e2e_s
 
     if rank == 0:
         avg_kern_s = float(np.mean(kern_ms)) / 1e3
@@ -361,6 +376,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": w.kernel, "kernel_ms": float(np.mean(kern_ms)), "bytes_alg_per_cw": b_alg},
         }
+        if e2e is not None:
+            rec["mc_end_to_end"] = {"value": e2e, "unit": "codewords/s",
+                                    "what": "pcub_mc_run_bin: info bits + encode + channel + decode + counters, "
+                                            "all on device, same codewords"}
         if world == 1 and not a.no_cpu:
             rec["cpu_baseline"] = w.cpu_baseline()
         print(json.dumps(rec), flush=True)

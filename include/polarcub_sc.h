@@ -127,6 +127,27 @@ int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, i
  * m = p / s, (0.5, 0.5) when s = 0.  count values in, [count][2] f64 out. */
 int pcub_leaf_marginals(const double* leaf, int64_t count, double* marginals, void* stream);
 
+/* Device Monte-Carlo (encodeDecodeSimulation, BinaryPolarEncoderDecoder.py:328-387, as a
+ * batched pipeline).  Codeword g's draws come from Philox4x32-10 keyed by (seed, g), so
+ * the codewords [offset, offset + B) are identical whichever rank or chunk makes them.
+ *   pcub_mc_info     K uniform information bits per codeword -> [ceil(K/32)][B] words
+ *   pcub_mc_channel  codeword bits [ceil(N/32)][B] -> joint pairs [N][B][2] f64;
+ *                    channel 0 = BI-AWGN (param = sigma^2, BPSK 0 -> +1),
+ *                    channel 1 = BSC (param = p, makeBSC's table)
+ *   pcub_mc_count_errors  counters[0] += B, [1] += frame errors, [2] += bit errors
+ *   pcub_mc_run_bin  info -> encode -> channel -> decode -> count for codewords
+ *                    [offset, offset + count), chunk codewords at a time; counters
+ *                    (device u64[4]) accumulate; the caller zeroes them. */
+int pcub_mc_info(uint64_t seed, int64_t offset, int64_t B, int32_t K, uint32_t* info_words, void* stream);
+int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel, double param,
+                    const uint32_t* x_words, double* xy, void* stream);
+int pcub_mc_count_errors(const uint32_t* decoded_words, const uint32_t* sent_words, int64_t B, int32_t K,
+                         uint64_t* counters, void* stream);
+size_t pcub_mc_run_bin_workspace(int64_t chunk, int32_t log2N, int32_t K);
+int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int32_t log2N, int32_t channel, double param,
+                    const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K, int64_t chunk,
+                    uint64_t* counters, void* workspace, size_t workspace_bytes, void* stream);
+
 /* [B][nbits] u8 (0/1) -> ceil(nbits/32) x B words, and back. */
 int pcub_pack_bits(const uint8_t* bits, int64_t B, int32_t nbits, uint32_t* words, void* stream);
 int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits, uint8_t* bits, void* stream);

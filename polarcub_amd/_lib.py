@@ -77,6 +77,18 @@ def lib():
                                         _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p]
     L.pcub_leaf_marginals.restype = ctypes.c_int
     L.pcub_leaf_marginals.argtypes = [_c_void_p, _i64, _c_void_p, _c_void_p]
+    _u64 = ctypes.c_uint64
+    L.pcub_mc_info.restype = ctypes.c_int
+    L.pcub_mc_info.argtypes = [_u64, _i64, _i64, _i32, _c_void_p, _c_void_p]
+    L.pcub_mc_channel.restype = ctypes.c_int
+    L.pcub_mc_channel.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p, _c_void_p]
+    L.pcub_mc_count_errors.restype = ctypes.c_int
+    L.pcub_mc_count_errors.argtypes = [_c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p]
+    L.pcub_mc_run_bin_workspace.restype = ctypes.c_size_t
+    L.pcub_mc_run_bin_workspace.argtypes = [_i64, _i32, _i32]
+    L.pcub_mc_run_bin.restype = ctypes.c_int
+    L.pcub_mc_run_bin.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p, _i32, _i64,
+                                  _c_void_p, _c_void_p, ctypes.c_size_t, _c_void_p]
     if L.pcub_abi_version() != 1:
         raise ImportError("libpolarcub_hip.so ABI mismatch; rebuild with python -m polarcub_amd.build --force")
     _lib = L
@@ -88,7 +100,8 @@ EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_b
            "pcub_sc_decode_qary_workspace", "pcub_sc_decode_qary", "pcub_polar_encode_qary",
            "pcub_pack_bits", "pcub_unpack_bits", "pcub_transpose_pairs", "pcub_sc_deletion_supported",
            "pcub_sc_decode_deletion", "pcub_sc_leaf_bin_workspace", "pcub_sc_leaf_bin", "pcub_sc_leaf_deletion",
-           "pcub_leaf_marginals"]
+           "pcub_leaf_marginals", "pcub_mc_info", "pcub_mc_channel", "pcub_mc_count_errors",
+           "pcub_mc_run_bin_workspace", "pcub_mc_run_bin"]
 
 
 def check(rc, what):

@@ -1,0 +1,244 @@
+// sc_mc.hip -- device Monte-Carlo: information bits and channel outputs keyed by the
+// GLOBAL codeword index, and the error counters (gfx950) + C-ABI launchers.
+//
+// The reference's encodeDecodeSimulation (BinaryPolarEncoderDecoder.py:328-387)
+// draws information bits (`0 if rng.random() < 0.5 else 1`, :350-358) and the
+// channel from MT19937 streams, one trial after another.  On the GPU every
+// codeword g gets its own Philox4x32-10 stream keyed by (seed, g): the batch
+// [offset, offset + B) is the same whichever rank or chunk generates it, so a run
+// sharded over G GPUs decodes exactly the codewords of the 1-GPU run and the
+// summed counters match (tests/test_gpu_mc.py).  Statistically the draws follow
+// the reference's laws (uniform bits; BSC flips with probability p; BI-AWGN
+// y = (1 - 2x) + sigma z with z ~ N(0, 1) by Box-Muller); they are not
+// MT19937-identical -- exact reproduction of a reference run uses the host
+// driver (coding.encodeDecodeSimulation), which replays the reference's RNGs.
+#include <hip/hip_runtime.h>
+
+#include "polarcub_sc.h"
+#include "sc_common.h"
+
+using namespace pcub;
+
+namespace {
+
+constexpr int kMcBlock = 256;
+
+// Philox4x32-10 (Salmon et al., SC'11): counter (c0..c3), key (k0, k1).
+struct P4 {
+    uint32_t v[4];
+};
+
+PCUB_HD P4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+    constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)M0 * c0, p1 = (uint64_t)M1 * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+        k0 += W0;
+        k1 += W1;
+    }
+    return P4{{c0, c1, c2, c3}};
+}
+
+// streams inside one codeword's counter space
+constexpr uint32_t kStreamInfo = 0, kStreamChannel = 1;
+
+// uniform double in (0, 1] from 53 random bits
+PCUB_HD double u01(uint32_t hi, uint32_t lo) {
+    const uint64_t m = (((uint64_t)hi << 32) | lo) >> 11;
+    return ((double)m + 1.0) * (1.0 / 9007199254740992.0);
+}
+
+struct McArgs {
+    uint64_t seed;
+    long long offset;  // global index of codeword 0 of this batch
+    long long B;
+    int n;
+    int K;
+    int channel;       // 0 = BI-AWGN (param = sigma^2), 1 = BSC (param = p)
+    double param;
+};
+
+// K uniform information bits per codeword: word w of codeword g is Philox
+// output lane (w & 3) of counter (g, kStreamInfo, w >> 2).
+__global__ __launch_bounds__(kMcBlock) void k_mc_info(McArgs A, uint32_t* info) {
+    const long long b = (long long)blockIdx.x * kMcBlock + threadIdx.x;
+    if (b >= A.B) return;
+    const uint64_t g = (uint64_t)(A.offset + b);
+    const int W = (A.K + 31) / 32;
+    for (int w = 0; w < W; w += 4) {
+        const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamInfo, (uint32_t)(w >> 2), (uint32_t)A.seed,
+                            (uint32_t)(A.seed >> 32));
+        for (int j = 0; j < 4 && w + j < W; ++j) {
+            uint32_t v = r.v[j];
+            if (w + j == W - 1 && (A.K & 31)) v &= (1u << (A.K & 31)) - 1u;
+            info[(long long)(w + j) * A.B + b] = v;
+        }
+    }
+}
+
+// Channel outputs as joint pairs, native [N][B][2]: element i of codeword g uses
+// Philox counter (g, kStreamChannel, i).
+__global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_t* x, double2* xy) {
+    const long long e = (long long)blockIdx.x * kMcBlock + threadIdx.x;
+    const long long N = 1LL << A.n;
+    if (e >= N * A.B) return;
+    const long long i = e / A.B, b = e - i * A.B;
+    const uint64_t g = (uint64_t)(A.offset + b);
+    const uint32_t xb = (x[(i >> 5) * A.B + b] >> (i & 31)) & 1u;
+    const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)i, (uint32_t)A.seed,
+                        (uint32_t)(A.seed >> 32));
+    double2 o;
+    if (A.channel == 0) {
+        const double s2 = A.param;
+        const double z = sqrt(-2.0 * log(u01(r.v[0], r.v[1]))) * cos(6.283185307179586 * u01(r.v[2], r.v[3]));
+        const double y = (xb ? -1.0 : 1.0) + sqrt(s2) * z;
+        const double c = 0.5 / sqrt(6.283185307179586 * s2);
+        o.x = c * exp(-((y - 1.0) * (y - 1.0)) / (2.0 * s2));
+        o.y = c * exp(-((y + 1.0) * (y + 1.0)) / (2.0 * s2));
+    } else {
+        const double p = A.param;
+        const uint32_t yb = xb ^ (u01(r.v[0], r.v[1]) <= p ? 1u : 0u);
+        // makeBSC table probs[y][x] = [[.5(1-p), .5p], [.5p, .5(1-p)]]
+        const double hi = 0.5 * (1.0 - p), lo = 0.5 * p;
+        o.x = yb ? lo : hi;
+        o.y = yb ? hi : lo;
+    }
+    xy[e] = o;
+}
+
+// counters[0] += B, [1] += frame errors, [2] += bit errors (information bits)
+__global__ __launch_bounds__(kMcBlock) void k_mc_count(const uint32_t* dec, const uint32_t* sent, long long B, int W,
+                                                        unsigned long long* counters) {
+    __shared__ unsigned long long fe[kMcBlock / 64], be[kMcBlock / 64];
+    const long long b = (long long)blockIdx.x * kMcBlock + threadIdx.x;
+    unsigned long long f = 0, e = 0;
+    if (b < B) {
+        for (int w = 0; w < W; ++w) e += (unsigned long long)__builtin_popcount(dec[(long long)w * B + b] ^ sent[(long long)w * B + b]);
+        f = e ? 1ull : 0ull;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        f += __shfl_xor(f, o);
+        e += __shfl_xor(e, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        fe[threadIdx.x >> 6] = f;
+        be[threadIdx.x >> 6] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long tf = 0, tb = 0;
+        for (int i = 0; i < kMcBlock / 64; ++i) {
+            tf += fe[i];
+            tb += be[i];
+        }
+        atomicAdd(&counters[1], tf);
+        atomicAdd(&counters[2], tb);
+        if (blockIdx.x == 0) atomicAdd(&counters[0], (unsigned long long)B);
+    }
+}
+
+unsigned grid_of(long long work) { return (unsigned)((work + kMcBlock - 1) / kMcBlock); }
+
+}  // namespace
+
+extern "C" int pcub_mc_info(uint64_t seed, int64_t offset, int64_t B, int32_t K, uint32_t* info_words, void* stream) {
+    if (B < 0 || offset < 0 || K < 0 || (K > 0 && B > 0 && !info_words)) return PCUB_EINVAL;
+    if (B == 0 || K == 0) return 0;
+    McArgs A{seed, offset, B, 0, K, 0, 0.0};
+    hipLaunchKernelGGL(k_mc_info, dim3(grid_of(B)), dim3(kMcBlock), 0, (hipStream_t)stream, A, info_words);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel, double param,
+                               const uint32_t* x_words, double* xy, void* stream) {
+    if (B < 0 || offset < 0 || log2N < 0 || log2N > 24 || (channel != 0 && channel != 1)) return PCUB_EINVAL;
+    if (channel == 0 && !(param > 0.0)) return PCUB_EINVAL;
+    if (channel == 1 && !(param >= 0.0 && param <= 1.0)) return PCUB_EINVAL;
+    if (B == 0) return 0;
+    if (!x_words || !xy) return PCUB_EINVAL;
+    McArgs A{seed, offset, B, log2N, 0, channel, param};
+    hipLaunchKernelGGL(k_mc_channel, dim3(grid_of(((long long)1 << log2N) * B)), dim3(kMcBlock), 0,
+                       (hipStream_t)stream, A, x_words, (double2*)xy);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcub_mc_count_errors(const uint32_t* decoded_words, const uint32_t* sent_words, int64_t B, int32_t K,
+                                    uint64_t* counters, void* stream) {
+    if (B < 0 || K < 0 || !counters || (B > 0 && K > 0 && (!decoded_words || !sent_words))) return PCUB_EINVAL;
+    if (B == 0) return 0;
+    const int W = (K + 31) / 32;
+    if (W == 0) {
+        // no information bits: only the codeword count moves
+        hipLaunchKernelGGL(k_mc_count, dim3(1), dim3(kMcBlock), 0, (hipStream_t)stream, decoded_words, sent_words,
+                           (long long)B, 0, (unsigned long long*)counters);
+        return (int)hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_mc_count, dim3(grid_of(B)), dim3(kMcBlock), 0, (hipStream_t)stream, decoded_words, sent_words,
+                       (long long)B, W, (unsigned long long*)counters);
+    return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// mc_run: the whole Monte-Carlo pipeline for codewords [offset, offset + count)
+// in chunks -- information bits -> polar encoder -> channel -> SC decode ->
+// error counters -- all stream-ordered on the device.
+
+namespace {
+
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+struct McLayout {
+    size_t info, x, xy, dec, dws, total;
+};
+
+McLayout mc_layout(int64_t chunk, int32_t log2N, int32_t K) {
+    McLayout L;
+    const size_t N = (size_t)1 << log2N;
+    const size_t iw = (size_t)((K + 31) / 32 > 0 ? (K + 31) / 32 : 1);
+    const size_t nw = (N + 31) / 32;
+    L.info = 0;
+    L.x = L.info + align256(iw * chunk * 4);
+    L.xy = L.x + align256(nw * chunk * 4);
+    L.dec = L.xy + align256(N * chunk * 16);
+    L.dws = L.dec + align256(iw * chunk * 4);
+    L.total = L.dws + align256(pcub_sc_decode_bin_workspace(chunk, log2N));
+    return L;
+}
+
+}  // namespace
+
+extern "C" size_t pcub_mc_run_bin_workspace(int64_t chunk, int32_t log2N, int32_t K) {
+    if (chunk <= 0 || log2N < 0 || log2N > 20 || K < 0 || K > (1 << log2N)) return 0;
+    return mc_layout(chunk, log2N, K).total;
+}
+
+extern "C" int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int32_t log2N, int32_t channel,
+                               double param, const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K,
+                               int64_t chunk, uint64_t* counters, void* workspace, size_t workspace_bytes, void* stream) {
+    if (count < 0 || offset < 0 || chunk <= 0 || !counters || !frozen_mask || !frozen_val) return PCUB_EINVAL;
+    const McLayout L = mc_layout(chunk, log2N, K);
+    if (!workspace || workspace_bytes < L.total) return PCUB_EINVAL;
+    char* ws = (char*)workspace;
+    uint32_t* info = (uint32_t*)(ws + L.info);
+    uint32_t* x = (uint32_t*)(ws + L.x);
+    double* xy = (double*)(ws + L.xy);
+    uint32_t* dec = (uint32_t*)(ws + L.dec);
+    for (int64_t c0 = 0; c0 < count; c0 += chunk) {
+        const int64_t B = (count - c0) < chunk ? (count - c0) : chunk;
+        int rc;
+        if (K > 0 && (rc = pcub_mc_info(seed, offset + c0, B, K, info, stream))) return rc;
+        if ((rc = pcub_polar_encode_bin(info, B, log2N, frozen_mask, frozen_val, K, x, stream))) return rc;
+        if ((rc = pcub_mc_channel(seed, offset + c0, B, log2N, channel, param, x, xy, stream))) return rc;
+        if ((rc = pcub_sc_decode_bin(xy, B, log2N, frozen_mask, frozen_val, K, dec, nullptr, nullptr, ws + L.dws,
+                                     L.total - L.dws, stream)))
+            return rc;
+        if ((rc = pcub_mc_count_errors(dec, info, B, K, counters, stream))) return rc;
+    }
+    return 0;
+}

@@ -101,3 +101,41 @@ def qsc_batch(code, B, p, generator, chunk=1 << 16):
         x = sc.encode_qary(code, inf)  # [b, N]
         xy[:, b0:b1, :] = channel.qsc_pairs_native(x.t(), code.q, p, generator=generator)
     return xy, info
+
+
+# ----------------------------------------------------------------------------- device Monte-Carlo (Philox)
+# Codeword g's information bits and channel draws are keyed by (seed, g): a batch
+# [offset, offset + B) is identical whichever rank / chunk generates it.
+
+CHANNEL_AWGN, CHANNEL_BSC = 0, 1
+
+
+def philox_batch(code, seed, offset, B, channel, param):
+    """Information words [ceil(K/32), B] and channel pairs [N, B, 2] for global codewords
+    [offset, offset + B) (pcub_mc_info -> pcub_polar_encode_bin -> pcub_mc_channel)."""
+    from . import _lib
+    L = _lib.lib()
+    dev = code.device
+    info = torch.zeros((max(1, code.info_words), B), dtype=torch.int32, device=dev)
+    _lib.check(L.pcub_mc_info(int(seed), int(offset), B, code.K, sc._p(info), sc._stream()), "pcub_mc_info")
+    x = sc.encode_native(code, info)
+    xy = torch.empty((code.N, B, 2), dtype=torch.float64, device=dev)
+    _lib.check(L.pcub_mc_channel(int(seed), int(offset), B, code.n, int(channel), float(param), sc._p(x), sc._p(xy),
+                                 sc._stream()), "pcub_mc_channel")
+    return info, xy
+
+
+def run_bin(code, seed, offset, count, channel, param, chunk=1 << 18):
+    """encodeDecodeSimulation as one device pipeline (pcub_mc_run_bin) over global codewords
+    [offset, offset + count); returns [codewords, frame errors, bit errors, 0]."""
+    from . import _lib
+    L = _lib.lib()
+    chunk = int(max(1, min(chunk, count)))
+    need = int(L.pcub_mc_run_bin_workspace(chunk, code.n, code.K))
+    ws = torch.empty(max(need, 16), dtype=torch.uint8, device=code.device)
+    counters = torch.zeros(4, dtype=torch.int64, device=code.device)
+    rc = L.pcub_mc_run_bin(int(seed), int(offset), int(count), code.n, int(channel), float(param),
+                           sc._p(code.fmask_dev), sc._p(code.fval_dev), code.K, chunk, sc._p(counters), sc._p(ws),
+                           ws.numel(), sc._stream())
+    _lib.check(rc, "pcub_mc_run_bin")
+    return [int(v) for v in counters.tolist()]

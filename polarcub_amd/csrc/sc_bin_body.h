@@ -464,7 +464,7 @@ struct SubWin {
     static constexpr int NW = SU > 64 ? SU / 64 : 1;
     static constexpr int SUW = SU > 64 ? 64 : SU;  // bits per window
     static constexpr uint64_t WMASK = (SUW == 64) ? ~0ull : ((1ull << SUW) - 1ull);
-    static_assert(SU <= 256, "at most four windows");
+    static_assert(SU <= 512, "at most eight windows");
 
     // decisions of the subtree from its S level-D values
     static PCUB_HD uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm, const uint64_t* fv, int lane) {
@@ -479,9 +479,9 @@ template <int S, int G, bool LDS = false, int NT = 0>
 PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
                              Lvl last = Lvl{nullptr, 0}) {
     static_assert(S == 8 || S == 16 || S == 32, "register subtree must fit one Y word");
-    static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lanes per codeword");
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per codeword");
     constexpr int s = (S == 8) ? 3 : (S == 16) ? 4 : 5;
-    constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : (G == 4) ? 2 : 3;
+    constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : (G == 4) ? 2 : (G == 8) ? 3 : 4;
     constexpr uint32_t SMASK = (S == 32) ? 0xffffffffu : ((1u << S) - 1u);
     constexpr int SU = S * G;  // real u positions per register subtree (<= 128)
     using W = SubWin<S, G>;

@@ -10,6 +10,7 @@ BinKernFn bin_kernel_part1(int v) {
         case 9: return k_sc_bin<8, 8, 4, false, 1>;
         case 13: return k_sc_bin<16, 4, 4, false, 1>;
         case 17: return k_sc_bin<32, 4, 3, false, 1>;
+        case 21: return k_sc_bin<32, 16, 2, false, 1>;
         default: return nullptr;
     }
 }

@@ -10,6 +10,7 @@ BinKernFn bin_kernel_part2(int v) {
         case 10: return k_sc_bin<16, 4, 2, false, 1>;
         case 14: return k_sc_bin<8, 4, 4, false, 1>;
         case 18: return k_sc_bin<32, 2, 3, false, 1>;
+        case 22: return k_sc_bin<32, 16, 3, false, 1>;
         default: return nullptr;
     }
 }

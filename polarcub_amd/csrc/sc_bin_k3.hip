@@ -10,6 +10,7 @@ BinKernFn bin_kernel_part3(int v) {
         case 11: return k_sc_bin<8, 4, 4, true, 0>;
         case 15: return k_sc_bin<32, 4, 2, false, 1>;
         case 19: return k_sc_bin<32, 8, 2, false, 1>;
+        case 23: return k_sc_bin<16, 16, 3, false, 1>;
         default: return nullptr;
     }
 }

@@ -178,12 +178,16 @@ PCUB_HD uint64_t gather_stride(uint64_t x) {
         x = (x | (x >> 6)) & 0x000F000F000F000Full;
         x = (x | (x >> 12)) & 0x000000FF000000FFull;
         return (x | (x >> 24)) & 0x000000000000FFFFull;
-    } else {
-        static_assert(G == 8, "lanes per codeword");
+    } else if constexpr (G == 8) {
         x &= 0x0101010101010101ull;
         x = (x | (x >> 7)) & 0x0003000300030003ull;
         x = (x | (x >> 14)) & 0x0000000F0000000Full;
         return (x | (x >> 28)) & 0x00000000000000FFull;
+    } else {
+        static_assert(G == 16, "lanes per codeword");
+        x &= 0x0001000100010001ull;
+        x = (x | (x >> 15)) & 0x0000000300000003ull;
+        return (x | (x >> 30)) & 0x000000000000000Full;
     }
 }
 

@@ -148,14 +148,12 @@ struct DelNode {
         using Cap = DelCap<L>;
         if constexpr (LEN == 2) {
             // children are length-1 trellises collapsed to memoryless rows
-            // (CollectionOfBinaryTrellises.py:68-82), then normalised by the decoder
-            Trel<1, Cap::V, Cap::E1> c;
+            // (CollectionOfBinaryTrellises.py:68-82), then normalised by the decoder;
+            // the collapse marginal is accumulated without building the child
             double m0, m1;
-            trellis_transform<2>(t, c, nullptr);
-            trellis_marginal(c, m0, m1);
+            trellis_collapse(t, nullptr, m0, m1);
             const uint32_t xm = cx.subtree(norm_pack(m0, m1));
-            trellis_transform<2>(t, c, &xm);
-            trellis_marginal(c, m0, m1);
+            trellis_collapse(t, &xm, m0, m1);
             const uint32_t xp = cx.subtree(norm_pack(m0, m1));
             return (xm ^ xp) | (xp << 1);
         } else {

@@ -139,9 +139,7 @@ __global__ __launch_bounds__(kLBlock) void k_sc_leaf(LeafArgs A) {
 }
 
 // compact leaf -> the reference's marginal: s = 0 + p0 + p1; m = p / s, or (0.5, 0.5)
-__global__ __launch_bounds__(kLBlock) void k_leaf_marginals(const double* leaf, long long count, double* m) {
-    const long long i = (long long)blockIdx.x * kLBlock + threadIdx.x;
-    if (i >= count) return;
+__device__ void leaf_marginal(const double* leaf, long long i, double* m) {
     const CV c = cv_load(leaf[i]);
     double p0 = c.s ? c.r : 1.0, p1 = c.s ? 1.0 : c.r;
     if (c.r != c.r) p0 = p1 = 0.0;  // the (0, 0) sentinel
@@ -150,6 +148,12 @@ __global__ __launch_bounds__(kLBlock) void k_leaf_marginals(const double* leaf, 
     s += p1;
     m[2 * i] = s > 0.0 ? p0 / s : 0.5;
     m[2 * i + 1] = s > 0.0 ? p1 / s : 0.5;
+}
+
+// grid-stride: count = N * B can pass the 32-bit dispatch grid size
+__global__ __launch_bounds__(kLBlock) void k_leaf_marginals(const double* leaf, long long count, double* m) {
+    for (long long i = (long long)blockIdx.x * kLBlock + threadIdx.x; i < count; i += (long long)gridDim.x * kLBlock)
+        leaf_marginal(leaf, i, m);
 }
 
 long long leaf_grid(long long B) {
@@ -209,7 +213,8 @@ extern "C" int pcub_sc_leaf_bin(const double* xy, int64_t B, int32_t log2N, cons
 extern "C" int pcub_leaf_marginals(const double* leaf, int64_t count, double* marginals, void* stream) {
     if (count < 0 || (count > 0 && (!leaf || !marginals))) return PCUB_EINVAL;
     if (count == 0) return 0;
-    hipLaunchKernelGGL(k_leaf_marginals, dim3((unsigned)((count + kLBlock - 1) / kLBlock)), dim3(kLBlock), 0,
+    const long long blocks = (count + kLBlock - 1) / kLBlock;
+    hipLaunchKernelGGL(k_leaf_marginals, dim3((unsigned)(blocks < (1 << 20) ? blocks : (1 << 20))), dim3(kLBlock), 0,
                        (hipStream_t)stream, leaf, (long long)count, marginals);
     return (int)hipGetLastError();
 }

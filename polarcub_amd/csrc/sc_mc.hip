@@ -84,10 +84,7 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_info(McArgs A, uint32_t* info) 
 
 // Channel outputs as joint pairs, native [N][B][2]: element i of codeword g uses
 // Philox counter (g, kStreamChannel, i).
-__global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_t* x, double2* xy) {
-    const long long e = (long long)blockIdx.x * kMcBlock + threadIdx.x;
-    const long long N = 1LL << A.n;
-    if (e >= N * A.B) return;
+__device__ void mc_channel_elem(const McArgs& A, const uint32_t* x, double2* xy, long long e) {
     const long long i = e / A.B, b = e - i * A.B;
     const uint64_t g = (uint64_t)(A.offset + b);
     const uint32_t xb = (x[(i >> 5) * A.B + b] >> (i & 31)) & 1u;
@@ -110,6 +107,13 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_
         o.y = yb ? hi : lo;
     }
     xy[e] = o;
+}
+
+// grid-stride: the dispatch packet's grid size is 32-bit (N * B reaches 2^32 at N = 4096, B = 2^20)
+__global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_t* x, double2* xy) {
+    const long long total = (1LL << A.n) * A.B;
+    for (long long e = (long long)blockIdx.x * kMcBlock + threadIdx.x; e < total; e += (long long)gridDim.x * kMcBlock)
+        mc_channel_elem(A, x, xy, e);
 }
 
 // counters[0] += B, [1] += frame errors, [2] += bit errors (information bits)
@@ -144,6 +148,10 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_count(const uint32_t* dec, cons
 }
 
 unsigned grid_of(long long work) { return (unsigned)((work + kMcBlock - 1) / kMcBlock); }
+unsigned stride_grid(long long work) {
+    const long long g = (work + kMcBlock - 1) / kMcBlock;
+    return (unsigned)(g < (1 << 20) ? g : (1 << 20));
+}
 
 }  // namespace
 
@@ -163,7 +171,7 @@ extern "C" int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t
     if (B == 0) return 0;
     if (!x_words || !xy) return PCUB_EINVAL;
     McArgs A{seed, offset, B, log2N, 0, channel, param};
-    hipLaunchKernelGGL(k_mc_channel, dim3(grid_of(((long long)1 << log2N) * B)), dim3(kMcBlock), 0,
+    hipLaunchKernelGGL(k_mc_channel, dim3(stride_grid(((long long)1 << log2N) * B)), dim3(kMcBlock), 0,
                        (hipStream_t)stream, A, x_words, (double2*)xy);
     return (int)hipGetLastError();
 }

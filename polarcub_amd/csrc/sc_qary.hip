@@ -10,183 +10,45 @@
 //   leaf   s = sum as above; m = p/s (or 1/q); u = first argmax(m)                  (:69-90, :342)
 //   frozen symbols are 0 (:347-351); the a-priori tree is never consulted.
 //   combine x[2h] = (xm+xp)%q, x[2h+1] = (q-xp)%q                                    (:397-399)
-// Storage follows the binary kernel: half-split order inside each node, so
-// children are op(in[p], in[p+L/2]) and the node's symbols are
-// y = [(ym+yp)%q | (q-yp)%q]; one codeword per lane; levels 1..n-2 in a
-// per-slot scratch (q doubles per position, slot-minor), the last node of two
-// positions in registers; decided symbols in a per-slot byte array.
+// The per-codeword schedule (register subtrees, fused chain passes, rate-0
+// skipping) is in sc_qary_body.h; this file owns the launch geometry: one
+// codeword per lane, 256-thread workgroups, a resident grid striding over
+// 256-codeword tiles so the per-slot stage buffers are reused.
 #include <hip/hip_runtime.h>
 
 #include "polarcub_sc.h"
-#include "sc_common.h"
+#include "sc_qary_body.h"
 
 using namespace pcub;
 
 namespace {
 
 constexpr int kQBlock = 256;
+constexpr int kQWaves = 3;  // waves per SIMD the register allocation must allow (3 workgroups per CU)
 
-template <int Q>
-struct QV {
-    double p[Q];
-};
-
-template <int Q>
-PCUB_HD QV<Q> q_normalize(QV<Q> v) {
-    double t = 0.0;
-#pragma unroll
-    for (int x = 0; x < Q; ++x) t = t + v.p[x];
-    if (t != 0.0) {
-#pragma unroll
-        for (int x = 0; x < Q; ++x) v.p[x] = v.p[x] / t;
-    }
-    return v;
-}
-
-template <int Q>
-PCUB_HD QV<Q> q_minus(const QV<Q>& a, const QV<Q>& b) {
-    QV<Q> o;
-#pragma unroll
-    for (int u = 0; u < Q; ++u) o.p[u] = 0.0;
-#pragma unroll
-    for (int x1 = 0; x1 < Q; ++x1)
-#pragma unroll
-        for (int x2 = 0; x2 < Q; ++x2) {
-            const int u1 = (x1 + x2) % Q;
-            o.p[u1] = o.p[u1] + a.p[x1] * b.p[x2];
-        }
-    return q_normalize<Q>(o);
-}
-
-template <int Q>
-PCUB_HD QV<Q> q_plus(const QV<Q>& a, const QV<Q>& b, int u1) {
-    QV<Q> o;
-#pragma unroll
-    for (int u2 = 0; u2 < Q; ++u2) {
-        // a[(u1+u2)%Q] with a wave-divergent u1: select instead of indexing
-        const int x1 = (u1 + u2) % Q;
-        double ax = a.p[0];
-#pragma unroll
-        for (int x = 1; x < Q; ++x) ax = (x1 == x) ? a.p[x] : ax;
-        o.p[u2] = 0.0 + ax * b.p[(Q - u2) % Q];
-    }
-    return q_normalize<Q>(o);
-}
-
-template <int Q>
-PCUB_HD int q_leaf(const QV<Q>& v) {
-    double s = 0.0;
-#pragma unroll
-    for (int x = 0; x < Q; ++x) s = s + v.p[x];
-    int arg = 0;
-    double best = 0.0;
-#pragma unroll
-    for (int x = 0; x < Q; ++x) {
-        const double m = (s > 0.0) ? v.p[x] / s : 1.0 / (double)Q;
-        if (x == 0 || m > best) {
-            best = m;
-            arg = x;
-        }
-    }
-    return arg;
-}
-
-struct QArgs {
-    const double* xy;       // [N][B][Q]
-    long long B;
-    int n;
-    const uint8_t* frozen;  // [N] 0/1
-    uint8_t* info;          // [K][B]
-    uint8_t* xhat;          // [N][B] or null
-    double* scratch;        // [(N - 2) positions][Q][nslots]
-    uint8_t* ysym;          // [N][nslots]
-    long long nslots;
-};
-
-template <int Q>
-PCUB_HD QV<Q> load_q(const double* base, long long pos, long long stride) {
-    QV<Q> v;
-#pragma unroll
-    for (int x = 0; x < Q; ++x) v.p[x] = base[(pos * Q + x) * stride];
-    return v;
-}
-
-template <int Q>
-PCUB_HD void store_q(double* base, long long pos, long long stride, const QV<Q>& v) {
-#pragma unroll
-    for (int x = 0; x < Q; ++x) base[(pos * Q + x) * stride] = v.p[x];
-}
-
-// depth-d node values at scratch positions [off(d), off(d) + (N >> d)), off(d) = N - 2*(N >> d) (d >= 1)
-template <int Q>
-PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store) {
-    const int n = A.n;
-    const int N = 1 << n;
-    const long long B = A.B, ns = A.nslots;
-    const double* in = A.xy + cw * Q;  // element i, symbol x at in[(i*B)*Q + x]
-    double* scr = A.scratch + slot;
-    uint8_t* Y = A.ysym + slot;
-    const int D = n - 1;  // depth of the 2-position nodes held in registers
-    int infow = 0;
-    for (int k = 0; k < (1 << D); ++k) {
-        const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
-        for (int d = d0; d <= D; ++d) {
-            const bool gop = (d == d0) && (k != 0);
-            const int Lo = N >> d;
-            const int ystart = (k >> (D - d + 1)) * (N >> (d - 1));  // minus child's first u position
-            for (int p = 0; p < Lo; ++p) {
-                QV<Q> a, b;
-                if (d == 1) {
-                    const long long i0 = 2 * (long long)bitrev((uint32_t)p, n - 1);  // natural rows (2q, 2q+1)
-                    a = load_q<Q>(in, i0 * B, 1);
-                    b = load_q<Q>(in, (i0 + 1) * B, 1);
-                } else {
-                    const long long off = (long long)N - 2 * (N >> (d - 1));
-                    a = load_q<Q>(scr, off + p, ns);
-                    b = load_q<Q>(scr, off + p + Lo, ns);
-                }
-                const QV<Q> o = gop ? q_plus<Q>(a, b, Y[(long long)(ystart + p) * ns]) : q_minus<Q>(a, b);
-                store_q<Q>(scr, (long long)N - 2 * Lo + p, ns, o);
-            }
-        }
-        // node of length 2 at depth D (positions off(D), off(D)+1)
-        const long long offD = (long long)N - 4;
-        const QV<Q> a = load_q<Q>(scr, offD, ns), b = load_q<Q>(scr, offD + 1, ns);
-        const int u0i = 2 * k, u1i = 2 * k + 1;
-        const int u0 = A.frozen[u0i] ? 0 : q_leaf<Q>(q_minus<Q>(a, b));
-        const int u1 = A.frozen[u1i] ? 0 : q_leaf<Q>(q_plus<Q>(a, b, u0));
-        if (store) {
-            if (!A.frozen[u0i]) A.info[(long long)(infow++) * B + cw] = (uint8_t)u0;
-            if (!A.frozen[u1i]) A.info[(long long)(infow++) * B + cw] = (uint8_t)u1;
-        } else {
-            infow += (A.frozen[u0i] ? 0 : 1) + (A.frozen[u1i] ? 0 : 1);
-        }
-        Y[(long long)u0i * ns] = (uint8_t)((u0 + u1) % Q);
-        Y[(long long)u1i * ns] = (uint8_t)((Q - u1) % Q);
-        // combine completed plus children: [(ym+yp)%q | (q-yp)%q]
-        for (int d = D; d >= 1 && ((k >> (D - d)) & 1); --d) {
-            const int Lc = N >> d;
-            const long long st = (long long)(k >> (D - d + 1)) * 2 * Lc;
-            for (int p = 0; p < Lc; ++p) {
-                const int ym = Y[(st + p) * ns], yp = Y[(st + Lc + p) * ns];
-                Y[(st + p) * ns] = (uint8_t)((ym + yp) % Q);
-                Y[(st + Lc + p) * ns] = (uint8_t)((Q - yp) % Q);
-            }
-        }
-    }
-    if (A.xhat && store)
-        for (int i = 0; i < N; ++i) A.xhat[(long long)i * B + cw] = Y[(long long)bitrev((uint32_t)i, n) * ns];
-}
-
-template <int Q>
-__global__ __launch_bounds__(kQBlock) void k_sc_qary(QArgs A) {
+template <int Q, int S>
+__global__ __launch_bounds__(kQBlock, kQWaves) void k_sc_qary(QArgs A) {
     const long long slot = (long long)blockIdx.x * kQBlock + threadIdx.x;
     const long long ntiles = (A.B + kQBlock - 1) / kQBlock;
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * kQBlock + threadIdx.x;
         const bool valid = cw < A.B;
-        decode_qary_cw<Q>(A, valid ? cw : A.B - 1, slot, valid);
+        decode_qary_cw<Q, S>(A, valid ? cw : A.B - 1, slot, valid);
     }
+}
+
+// rate-0 table: frozen bytes -> words -> first all-frozen depth per register subtree
+__global__ __launch_bounds__(kQBlock) void k_q_frozen_words(const uint8_t* frozen, int N, uint32_t* words) {
+    const int w = blockIdx.x * kQBlock + threadIdx.x;
+    if (w >= (N + 31) / 32) return;
+    uint32_t o = 0;
+    for (int t = 0; t < 32 && 32 * w + t < N; ++t) o |= (uint32_t)(frozen[32 * w + t] != 0) << t;
+    words[w] = o;
+}
+
+__global__ __launch_bounds__(kQBlock) void k_q_ef(const uint32_t* words, int D, int S, uint8_t* ef) {
+    const int k = blockIdx.x * kQBlock + threadIdx.x;
+    if (k < (1 << D)) ef[k] = (uint8_t)first_frozen_depth(words, k, D, S);
 }
 
 // q-ary encoder: u (info symbols at information positions, 0 at frozen ones)
@@ -218,24 +80,49 @@ __global__ __launch_bounds__(kQBlock) void k_encode_qary(const uint8_t* info, lo
 }
 
 typedef void (*QKern)(QArgs);
-QKern qkernel(int q) {
-    switch (q) {
-        case 2: return k_sc_qary<2>;
-        case 3: return k_sc_qary<3>;
-        case 4: return k_sc_qary<4>;
-        case 5: return k_sc_qary<5>;
-        case 6: return k_sc_qary<6>;
-        case 7: return k_sc_qary<7>;
-        case 8: return k_sc_qary<8>;
+
+// register positions per chain: 8 for q <= 4, 4 for q <= 8, at most N/2
+int q_regs(int q, int n) {
+    int S = q <= 4 ? 8 : 4;
+    while (S > 1 && (1 << n) < 2 * S) S >>= 1;
+    return S;
+}
+
+template <int Q>
+QKern qkernel_s(int S) {
+    switch (S) {
+        case 1: return k_sc_qary<Q, 1>;
+        case 2: return k_sc_qary<Q, 2>;
+        case 4: return k_sc_qary<Q, 4>;
+        case 8:
+            if constexpr (Q <= 4) return k_sc_qary<Q, 8>;
+            else return nullptr;
         default: return nullptr;
     }
 }
 
-long long qgrid(long long B, int q) {
+QKern qkernel(int q, int n) {
+    const int S = q_regs(q, n);
+    switch (q) {
+        case 2: return qkernel_s<2>(S);
+        case 3: return qkernel_s<3>(S);
+        case 4: return qkernel_s<4>(S);
+        case 5: return qkernel_s<5>(S);
+        case 6: return qkernel_s<6>(S);
+        case 7: return qkernel_s<7>(S);
+        case 8: return qkernel_s<8>(S);
+        default: return nullptr;
+    }
+}
+
+long long qgrid(long long B, int q, int n) {
     int dev = 0, cus = 0, occ = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, qkernel(q), kQBlock, 0) != hipSuccess || occ < 1) occ = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, qkernel(q, n), kQBlock, 0) != hipSuccess || occ < 1) occ = 1;
+    // the launch bounds guarantee kQWaves resident workgroups per CU (the occupancy
+    // query reports 1 for these kernels on ROCm 7.2)
+    if (occ < kQWaves) occ = kQWaves;
     const long long ntiles = (B + kQBlock - 1) / kQBlock;
     const long long g = (long long)cus * occ;
     return ntiles < g ? ntiles : g;
@@ -243,40 +130,58 @@ long long qgrid(long long B, int q) {
 
 size_t qslot_bytes(int n, int q) {
     const size_t N = (size_t)1 << n;
-    return (N - 2) * q * sizeof(double) + N;
+    const size_t S = (size_t)q_regs(q, n);
+    return (N - 2 * S) * q * sizeof(double) + N;
+}
+
+// rate-0 table + packed frozen words, ahead of the slots
+size_t qtable_bytes(int n, int q) {
+    const int D = n - __builtin_ctz((unsigned)q_regs(q, n));
+    return ((((size_t)1 << n) + 31) / 32 * 4 + ((size_t)1 << D) + 255) & ~(size_t)255;
 }
 
 }  // namespace
 
 extern "C" size_t pcub_sc_decode_qary_workspace(int64_t B, int32_t log2N, int32_t q) {
-    if (B <= 0 || log2N < 2 || log2N > 20 || !qkernel(q)) return 0;
-    return (size_t)qgrid(B, q) * kQBlock * qslot_bytes(log2N, q);
+    if (B <= 0 || log2N < 2 || log2N > 20 || !qkernel(q, log2N)) return 0;
+    return qtable_bytes(log2N, q) + (size_t)qgrid(B, q, log2N) * kQBlock * qslot_bytes(log2N, q);
 }
 
 extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, int32_t q, const uint8_t* frozen,
                                    int32_t K, uint8_t* info, uint8_t* xhat, void* workspace, size_t workspace_bytes,
                                    void* stream) {
-    if (B < 0 || log2N < 2 || log2N > 20 || !qkernel(q) || !frozen) return PCUB_EINVAL;
+    if (B < 0 || log2N < 2 || log2N > 20 || !qkernel(q, log2N) || !frozen) return PCUB_EINVAL;
     if (K < 0 || K > (1 << log2N) || (K > 0 && !info) || (B > 0 && !xy)) return PCUB_EINVAL;
     if (B == 0) return 0;
-    long long g = qgrid(B, q);
+    long long g = qgrid(B, q, log2N);
     if (g <= 0) return (int)hipErrorNoDevice;
     const size_t per_block = (size_t)kQBlock * qslot_bytes(log2N, q);
-    if (!workspace) return PCUB_EINVAL;
-    if ((size_t)g * per_block > workspace_bytes) g = (long long)(workspace_bytes / per_block);
-    if (g <= 0) return PCUB_EINVAL;
+    const size_t tb = qtable_bytes(log2N, q);
+    if (!workspace || workspace_bytes < tb + per_block) return PCUB_EINVAL;
+    if ((size_t)g * per_block > workspace_bytes - tb) g = (long long)((workspace_bytes - tb) / per_block);
+    const int N = 1 << log2N;
+    const int S = q_regs(q, log2N);
+    const int D = log2N - __builtin_ctz((unsigned)S);
+    hipStream_t st = (hipStream_t)stream;
+    uint32_t* words = (uint32_t*)workspace;
+    uint8_t* ef = (uint8_t*)workspace + ((size_t)N + 31) / 32 * 4;
+    hipLaunchKernelGGL(k_q_frozen_words, dim3((unsigned)(((N + 31) / 32 + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0, st,
+                       frozen, N, words);
+    hipLaunchKernelGGL(k_q_ef, dim3((unsigned)(((1 << D) + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0, st, words, D, S,
+                       ef);
     QArgs A;
     A.xy = xy;
     A.B = B;
     A.n = log2N;
     A.frozen = frozen;
+    A.ef = ef;
     A.info = info;
     A.xhat = xhat;
     A.nslots = g * kQBlock;
-    const size_t N = (size_t)1 << log2N;
-    A.scratch = (double*)workspace;
-    A.ysym = (uint8_t*)workspace + (size_t)A.nslots * (N - 2) * q * sizeof(double);
-    hipLaunchKernelGGL(qkernel(q), dim3((unsigned)g), dim3(kQBlock), 0, (hipStream_t)stream, A);
+    char* slots = (char*)workspace + tb;
+    A.scratch = (double*)slots;
+    A.ysym = (uint8_t*)slots + (size_t)A.nslots * (N - 2 * S) * q * sizeof(double);
+    hipLaunchKernelGGL(qkernel(q, log2N), dim3((unsigned)g), dim3(kQBlock), 0, st, A);
     return (int)hipGetLastError();
 }
 

@@ -71,26 +71,39 @@ __global__ __launch_bounds__(kEncBlock) void k_encode_bin(const uint32_t* __rest
     }
 }
 
+// Element-wise kernels stride over their index space: the dispatch packet's grid
+// size is 32-bit, so a grid of one thread per element would overflow at 2^32.
+constexpr long long kMaxGridBlocks = 1 << 20;
+
 __global__ void k_pack_bits(const uint8_t* __restrict__ bits, long long B, int nbits, uint32_t* __restrict__ words) {
     const int W = (nbits + 31) / 32;
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long long)W * B) return;
-    const long long b = idx % B;
-    const int w = (int)(idx / B);
-    uint32_t o = 0;
-    for (int t = 0; t < 32; ++t) {
-        const int i = 32 * w + t;
-        if (i < nbits) o |= (uint32_t)(bits[b * nbits + i] & 1u) << t;
+    const long long total = (long long)W * B;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long b = idx % B;
+        const int w = (int)(idx / B);
+        uint32_t o = 0;
+        for (int t = 0; t < 32; ++t) {
+            const int i = 32 * w + t;
+            if (i < nbits) o |= (uint32_t)(bits[b * nbits + i] & 1u) << t;
+        }
+        words[idx] = o;
     }
-    words[idx] = o;
 }
 
 __global__ void k_unpack_bits(const uint32_t* __restrict__ words, long long B, int nbits, uint8_t* __restrict__ bits) {
-    const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long long)nbits * B) return;
-    const long long b = idx / nbits;
-    const int i = (int)(idx % nbits);
-    bits[idx] = (uint8_t)((words[(long long)(i >> 5) * B + b] >> (i & 31)) & 1u);
+    const long long total = (long long)nbits * B;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long b = idx / nbits;
+        const int i = (int)(idx % nbits);
+        bits[idx] = (uint8_t)((words[(long long)(i >> 5) * B + b] >> (i & 31)) & 1u);
+    }
+}
+
+unsigned stride_grid(long long total, int block) {
+    const long long g = (total + block - 1) / block;
+    return (unsigned)(g < kMaxGridBlocks ? g : kMaxGridBlocks);
 }
 
 // [B][N][q] -> [N][B][q] through a 32 (codewords) x 16 (positions) LDS tile, q <= 8.
@@ -136,7 +149,7 @@ extern "C" int pcub_pack_bits(const uint8_t* bits, int64_t B, int32_t nbits, uin
     if (B < 0 || nbits < 0 || (B > 0 && nbits > 0 && (!bits || !words))) return PCUB_EINVAL;
     const long long total = (long long)((nbits + 31) / 32) * B;
     if (total == 0) return 0;
-    hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, bits,
+    hipLaunchKernelGGL(k_pack_bits, dim3(stride_grid(total, 256)), dim3(256), 0, (hipStream_t)stream, bits,
                        (long long)B, nbits, words);
     return (int)hipGetLastError();
 }
@@ -145,7 +158,7 @@ extern "C" int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits,
     if (B < 0 || nbits < 0 || (B > 0 && nbits > 0 && (!bits || !words))) return PCUB_EINVAL;
     const long long total = (long long)nbits * B;
     if (total == 0) return 0;
-    hipLaunchKernelGGL(k_unpack_bits, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, words,
+    hipLaunchKernelGGL(k_unpack_bits, dim3(stride_grid(total, 256)), dim3(256), 0, (hipStream_t)stream, words,
                        (long long)B, nbits, bits);
     return (int)hipGetLastError();
 }

@@ -174,6 +174,40 @@ PCUB_HD void trellis_marginal(const T& t, double& m0, double& m1) {
     }
 }
 
+// The collapse of a length-2 trellis (CollectionOfBinaryTrellises.py:68-82): its
+// minus/plus child has length 1, and with no guard-band ones its only vertices are
+// the start (vpos 0) and the end (vpos m), so the child has at most two edges,
+// start -> end with label 0 and with label 1.  The child's marginal (normalize=False)
+// is therefore 0.0 + the accumulated probability of each of those edges, i.e. the
+// sum of the transform's contributions per label in the transform's iteration
+// order -- accumulated here directly, without materialising the child.
+template <class P>
+PCUB_HD void trellis_collapse(const P& pt, const uint32_t* dec, double& m0, double& m1) {
+    m0 = 0.0;
+    m1 = 0.0;
+    const int dj = dec ? (int)(*dec & 1u) : 0;
+    for (int wi = 0; wi < pt.nv[1]; ++wi) {
+        const int w = pt.vp[1][wi];
+        for (int a = 0; a < pt.ne[0]; ++a) {
+            const uint32_t ka = pt.key[0][a];
+            if (ek_to(ka) != w) continue;
+            for (int b = 0; b < pt.ne[1]; ++b) {
+                const uint32_t kb = pt.key[1][b];
+                if (ek_from(kb) != w) continue;
+                const double prob = pt.p[0][a] * pt.p[1][b];
+                const int ml = ek_lbl(ka) ^ ek_lbl(kb);
+                int x = ml;
+                if (dec) {
+                    if (ml != dj) continue;
+                    x = ek_lbl(kb);
+                }
+                if (x) m1 += prob;
+                else m0 += prob;
+            }
+        }
+    }
+}
+
 // trimZerosAtEdges on word[s .. e): the first and last 1 (Guardbands.py:66-93).
 template <class BitF>
 PCUB_HD void trim_range(const BitF& bit, int& s, int& e) {

@@ -14,7 +14,7 @@ i=0
 for grp in "${P[@]}"; do
   i=$((i+1))
   cd /tmp
-  timeout -s KILL 120 rocprofv3 --pmc ${grp//,/ } --output-format csv -d $R/gpurun_out/sq_${TAG:-x}_$i -o pmc -- python3 $R/scripts/decode_only.py --batch ${BATCH:-1048576} --reps 1 ${DECODE_EXTRA:-} > $R/gpurun_out/sq_${TAG:-x}_$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc ${grp//,/ } --output-format csv -d $R/gpurun_out/sq_${TAG:-x}_$i -o pmc -- python3 ${PROFILED:-$R/scripts/decode_only.py --batch ${BATCH:-1048576} --reps 1 ${DECODE_EXTRA:-}} > $R/gpurun_out/sq_${TAG:-x}_$i.log 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"; cd $R
   [ $rc -eq 0 ] || exit $rc
 done

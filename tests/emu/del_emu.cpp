@@ -65,16 +65,23 @@ struct Node {
             std::vector<double> vals(T);
             for (size_t t = 0; t < T; ++t) {
                 double m0, m1;
+                trellis_collapse(ts[t], nullptr, m0, m1);
+                // the materialised child gives the same marginal (kernel shortcut check)
+                double c0, c1;
                 trellis_transform<2>(ts[t], c, nullptr);
-                trellis_marginal(c, m0, m1);
+                trellis_marginal(c, c0, c1);
+                if (as_bits(c0) != as_bits(m0) || as_bits(c1) != as_bits(m1)) throw 1;
                 vals[t] = norm_pack(m0, m1);
             }
             const std::vector<int> xm = mem_sc(vals, cx);
             for (size_t t = 0; t < T; ++t) {
                 double m0, m1;
                 const uint32_t d = (uint32_t)xm[t];
+                trellis_collapse(ts[t], &d, m0, m1);
+                double c0, c1;
                 trellis_transform<2>(ts[t], c, &d);
-                trellis_marginal(c, m0, m1);
+                trellis_marginal(c, c0, c1);
+                if (as_bits(c0) != as_bits(m0) || as_bits(c1) != as_bits(m1)) throw 1;
                 vals[t] = norm_pack(m0, m1);
             }
             const std::vector<int> xp = mem_sc(vals, cx);
@@ -135,11 +142,15 @@ extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, lon
         std::vector<int> xh;
         const uint8_t* w = rx + b * (long long)stride;
         const int len = rx_len[b];
-        switch (n0) {
-            case 1: decode_one<1>(w, len, n, pd, cx, xh); break;
-            case 2: decode_one<2>(w, len, n, pd, cx, xh); break;
-            case 3: decode_one<3>(w, len, n, pd, cx, xh); break;
-            default: return -1;
+        try {
+            switch (n0) {
+                case 1: decode_one<1>(w, len, n, pd, cx, xh); break;
+                case 2: decode_one<2>(w, len, n, pd, cx, xh); break;
+                case 3: decode_one<3>(w, len, n, pd, cx, xh); break;
+                default: return -1;
+            }
+        } catch (int) {
+            return -3;  // trellis_collapse disagrees with the materialised child's marginal
         }
         if ((int)cx.info.size() != K) return -2;
         for (int i = 0; i < K; ++i)

@@ -21,7 +21,7 @@ def sc():
     return _sc
 
 
-@pytest.mark.parametrize("variant", range(21))
+@pytest.mark.parametrize("variant", range(24))
 @pytest.mark.parametrize("name", BIN_SETS)
 def test_decode_matches_reference(sc, name, variant):
     sc.set_variant(variant)
@@ -48,7 +48,7 @@ def test_edge_cases(sc, idx, variant):
     assert np.array_equal(xhat.cpu().numpy(), c["xhat"])
 
 
-@pytest.mark.parametrize("variant", range(21))
+@pytest.mark.parametrize("variant", range(24))
 def test_ragged_batches_and_slot_reuse(sc, variant):
     """Batch sizes that are not tile multiples, and more tiles than resident slots."""
     from oracle import orc
@@ -68,7 +68,7 @@ def test_ragged_batches_and_slot_reuse(sc, variant):
     sc.set_variant()
 
 
-@pytest.mark.parametrize("variant", range(21))
+@pytest.mark.parametrize("variant", range(24))
 def test_rate0_blocks(sc, variant):
     """Frozen sets full of aligned rate-0 blocks (skipped by every variant's schedule,
     at the stage levels and inside the register and cross-lane subtrees)."""

@@ -19,15 +19,18 @@
 // (CollectionOfBinaryTrellises.py:58-66), and the re-encoding combine
 // (BinaryPolarEncoderDecoder.py:319-323) maps trellis t's slices onto itself.
 //
-// Each lane keeps one trellis per depth (the current SC path) in private memory;
-// the schedule is identical in every lane, only trip counts of the small edge
-// loops differ.  Received words are read straight from HBM (u8, row per
+// n0 = 2 (main_deletion.py's default shape at n = 8) runs on the register-resident
+// representation of trellis_n02.h (no per-lane memory at all); other n0 keep one
+// trellis per depth (the current SC path) in private memory (trellis_body.h).  The
+// schedule is identical in every lane, only trip counts of the small edge loops
+// differ.  Received words are read straight from HBM (u8, row per
 // codeword, a few hundred bytes each, L1/L2-resident while a group works on them).
 #include <hip/hip_runtime.h>
 
 #include "polarcub_sc.h"
 #include "sc_bin_body.h"
 #include "trellis_body.h"
+#include "trellis_n02.h"
 
 using namespace pcub;
 
@@ -83,7 +86,7 @@ struct XSubE {
 // Per-lane decoding context: frozen windows, decisions, information accumulator.
 template <int T, bool EXP>
 struct DelCtx {
-    const DelArgs* A;
+    DelArgs A;  // by value: taking the kernel argument's address would force it to scratch
     long long cw;
     bool leader;  // group position 0 stores the information words and exported leaves
     int lane;
@@ -104,14 +107,14 @@ struct DelCtx {
 
     // SC over the collapsed memoryless node (one compact value per lane); returns
     // this lane's bit of the node's re-encoded vector (natural position = its trellis).
-    __device__ uint32_t subtree(double v) {
-        const uint64_t fm = window(A->fmask);
-        const uint64_t fv = A->fval_cw ? window(A->fval_cw + cw, A->B) : window(A->fval);
+    __device__ __forceinline__ uint32_t subtree(double v) {
+        const uint64_t fm = window(A.fmask);
+        const uint64_t fv = A.fval_cw ? window(A.fval_cw + cw, A.B) : window(A.fval);
         uint64_t ub = 0;
         uint32_t y;
         constexpr uint64_t WM = (T == 64) ? ~0ull : ((1ull << T) - 1ull);
         if constexpr (EXP) {
-            y = XSubE<T, 0>::run(v, ub, fm, fv, lane, A->leaf + (long long)k * T * A->B + cw, A->B, leader) & 1u;
+            y = XSubE<T, 0>::run(v, ub, fm, fv, lane, A.leaf + (long long)k * T * A.B + cw, A.B, leader) & 1u;
         } else if (fm == WM) {  // rate-0 node: decisions are the frozen values
             ub = fv;
             y = frozen_local<1, T>(fv, lane & (T - 1));
@@ -121,7 +124,7 @@ struct DelCtx {
         for (uint64_t im = ~fm & WM; im != 0ull; im &= im - 1ull) {
             acc |= (uint32_t)((ub >> __builtin_ctzll(im)) & 1ull) << nacc;
             if (++nacc == 32) {
-                if (leader && A->info) A->info[(long long)infow * A->B + cw] = acc;
+                if (leader && A.info) A.info[(long long)infow * A.B + cw] = acc;
                 acc = 0;
                 nacc = 0;
                 ++infow;
@@ -174,6 +177,32 @@ struct DelNode {
     }
 };
 
+// n0 = 2: the two trellis levels on the register-resident representation
+// (trellis_n02.h); same recursion as DelNode.  Returns the 4-bit re-encoded slice.
+// one depth-1 node: minus (dec == nullptr) or plus child of the base trellis
+template <int T, bool EXP>
+__device__ __forceinline__ uint32_t del_n02_half(const Base02& b, const uint32_t* dec, DelCtx<T, EXP>& cx) {
+    Child02 c;
+    n02_transform(b, dec, c);
+    n02_normalize(c);
+    double m0, m1;
+    n02_collapse(c, nullptr, m0, m1);
+    const uint32_t xm = cx.subtree(norm_pack(m0, m1));
+    n02_collapse(c, &xm, m0, m1);
+    const uint32_t xp = cx.subtree(norm_pack(m0, m1));
+    return (xm ^ xp) | (xp << 1);
+}
+
+template <int T, bool EXP>
+__device__ __forceinline__ uint32_t del_n02(const Base02& b, DelCtx<T, EXP>& cx) {
+    const uint32_t ym = del_n02_half(b, nullptr, cx);
+    const uint32_t yp = del_n02_half(b, &ym, cx);
+    uint32_t x = 0;  // x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h]
+#pragma unroll
+    for (int h = 0; h < 2; ++h) x |= ((((ym ^ yp) >> h) & 1u) << (2 * h)) | (((yp >> h) & 1u) << (2 * h + 1));
+    return x;
+}
+
 template <int N0, int TB, bool EXP>
 __global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
     constexpr int L = 1 << N0;
@@ -200,11 +229,8 @@ __global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
     int s, m;
     segment_of(bit, len, TB, t, s, m);
 
-    Trel<L, Cap::V, Cap::E0> base;
-    trellis_build<L>(base, bit, s, m, A.pd);
-
     DelCtx<T, EXP> cx;
-    cx.A = &A;
+    cx.A = A;
     cx.cw = cw;
     cx.leader = valid && p == 0;
     cx.lane = lane;
@@ -212,7 +238,23 @@ __global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
     cx.acc = 0;
     cx.nacc = 0;
     cx.infow = 0;
-    const uint32_t x = DelNode<L, T, L, EXP>::run(base, cx);
+    uint32_t x;
+    if constexpr (N0 == 2) {
+        // register-resident path (trellis_n02.h): the base trellis is implicit
+        Base02 b;
+        b.m = m;
+        b.d = kN02L - m;
+        b.y = 0;
+        if (m <= kN02L)
+            for (int i = 0; i < m; ++i) b.y |= (uint32_t)(bit(s + i) & 1) << i;
+        b.pins = 0.5 * (1.0 - A.pd);
+        b.pdel = 0.5 * A.pd;
+        x = del_n02(b, cx);
+    } else {
+        Trel<L, Cap::V, Cap::E0> base;
+        trellis_build<L>(base, bit, s, m, A.pd);
+        x = DelNode<L, T, L, EXP>::run(base, cx);
+    }
     if (cx.nacc && cx.leader && A.info) A.info[(long long)cx.infow * A.B + cw] = cx.acc;
 
     // x_hat: trellis t's slice is natural positions [t*L, (t+1)*L)

@@ -1,0 +1,244 @@
+// trellis_n02.h -- register-resident trellis stages for n0 = 2 (4-input trellises,
+// the main_deletion.py configuration), host + device.
+//
+// Same computation as trellis_body.h (build -> minus/plus -> normalise -> collapse,
+// VectorDistributions/BinaryTrellis.py:206-438, CollectionOfBinaryTrellises.py:55-82),
+// with no per-lane memory:
+//   * the base trellis is never stored: its vertices, its edges and their creation
+//     order follow from (m, received bits, pd) -- buildTrellis_uniformInput_deletion
+//     (:384-436) walks layers in order and, inside a layer, the from-positions vp in
+//     ascending order, creating the insertion edge vp -> vp+1 (label y[vp]) and then the
+//     deletion edges vp -> vp (labels 0, 1).  So the out-edges of a vertex in dict
+//     order are [insertion, deletion 0, deletion 1], its in-edges [insertion from
+//     vp-1, deletion 0, deletion 1 from vp], and a layer's vertices are inserted in the
+//     order the previous layer's edges reach them;
+//   * the depth-1 trellis (2 inputs) has layers {0}, W (the vertices of base layer 2
+//     it reaches, at most 3) and {m}: at most 6 edges start -> w and 6 edges w -> end.
+//     It is kept in fixed-size arrays appended in creation order, accessed only with
+//     compile-time indices (fully unrolled, predicated), so it stays in VGPRs.
+// Sums keep the reference's iteration order exactly (tests/test_emulated_deletion.py
+// checks this path against the general one and the golden vectors).
+#pragma once
+#include "sc_common.h"
+
+namespace pcub {
+
+constexpr int kN02L = 4;  // inputs per base trellis
+constexpr int kN02V = 3;  // vertices per layer, at most
+constexpr int kN02E = 6;  // edges per depth-1 edge layer, at most
+
+// The base trellis of one segment (length m, received bits y: bit i = symbol s+i;
+// edges exist only when m <= 4).
+struct Base02 {
+    int m;
+    int d;        // deletions: 4 - m
+    uint32_t y;   // received bits (m <= 4)
+    double pins;  // 0.5 (1 - pd)
+    double pdel;  // 0.5 pd
+    PCUB_HD int lo(int l) const { return l - d > 0 ? l - d : 0; }
+    PCUB_HD int hi(int l) const { return l < m ? l : m; }
+    PCUB_HD bool from_ok(int l, int vp) const { return vp >= lo(l) && vp <= hi(l); }
+    // edges leaving (l, vp), creation order: kind 0 = insertion, 1 = deletion 0, 2 = deletion 1
+    PCUB_HD bool out_edge(int l, int vp, int kind, int& to, int& lbl, double& p) const {
+        if (!from_ok(l, vp)) return false;
+        if (kind == 0) {
+            if (vp >= m) return false;
+            to = vp + 1;
+            lbl = (int)((y >> vp) & 1u);
+            p = pins;
+            return true;
+        }
+        if (l + 1 - d > vp) return false;
+        to = vp;
+        lbl = kind - 1;
+        p = (kind == 1 && !(vp > 0 && vp < m)) ? 0.5 : pdel;
+        return true;
+    }
+    // vertex order of base layer l (1 <= l <= 3): the previous layer's edges reach them
+    // in creation order, then any from-position of layer l not reached yet
+    PCUB_HD int layer(int l, int* vs) const {
+        int c = 0;
+        auto add = [&](int v) {
+            bool have = false;
+#pragma unroll
+            for (int i = 0; i < kN02V; ++i) have = have || (i < c && vs[i] == v);
+            if (!have) {
+#pragma unroll
+                for (int i = 0; i < kN02V; ++i)
+                    if (i == c) vs[i] = v;
+                ++c;
+            }
+        };
+#pragma unroll
+        for (int s = 0; s < kN02V; ++s) {
+            const int vp = lo(l - 1) + s;
+            if (vp > hi(l - 1)) continue;
+            if (vp < m) add(vp + 1);
+            if (l - d <= vp) add(vp);
+        }
+#pragma unroll
+        for (int s = 0; s < kN02V; ++s) {
+            const int vp = lo(l) + s;
+            if (vp > hi(l)) continue;
+            if (vp < m || l + 1 - d <= vp) add(vp);
+        }
+        return c;
+    }
+};
+
+// depth-1 trellis: layers {0}, W, {m}
+struct Child02 {
+    int nw;
+    int w[kN02V];        // layer-1 vertices in insertion order
+    int n0;              // edges 0 -> w (creation order): key = w*2 + label
+    int k0[kN02E];
+    double p0[kN02E];
+    int n1;              // edges w -> m: key = w*2 + label
+    int k1[kN02E];
+    double p1[kN02E];
+
+    PCUB_HD void vertex(int v) {
+        bool have = false;
+#pragma unroll
+        for (int i = 0; i < kN02V; ++i) have = have || (i < nw && w[i] == v);
+        if (!have) {
+#pragma unroll
+            for (int i = 0; i < kN02V; ++i)
+                if (i == nw) w[i] = v;
+            ++nw;
+        }
+    }
+    // addToEdgeProb on edge layer J (BinaryTrellis.py:128-136): from-vertex, to-vertex, edge
+    template <int J>
+    PCUB_HD void add(int key, double p) {
+        int(&k)[kN02E] = J ? k1 : k0;
+        double(&pp)[kN02E] = J ? p1 : p0;
+        int& n = J ? n1 : n0;
+        bool found = false;
+#pragma unroll
+        for (int i = 0; i < kN02E; ++i)
+            if (i < n && k[i] == key) {
+                pp[i] += p;
+                found = true;
+            }
+        if (!found) {
+#pragma unroll
+            for (int i = 0; i < kN02E; ++i)
+                if (i == n) {
+                    k[i] = key;
+                    pp[i] = 0.0 + p;
+                }
+            ++n;
+        }
+    }
+};
+
+// minus (dec == nullptr) or plus (bits 0, 1 of *dec) transform of the base trellis
+// (BinaryTrellis.py:206-258) into the depth-1 trellis.
+PCUB_HD void n02_transform(const Base02& b, const uint32_t* dec, Child02& c) {
+    c.nw = c.n0 = c.n1 = 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int mid = 2 * j + 1;
+        const int dj = dec ? (int)((*dec >> j) & 1u) : 0;
+        int ws[kN02V];
+        const int nws = b.layer(mid, ws);
+#pragma unroll
+        for (int wi = 0; wi < kN02V; ++wi) {
+            if (wi >= nws) continue;
+            const int w = ws[wi];
+            // in-edges of w: insertion from w-1, then deletions 0, 1 from w (creation order)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const int u = a == 0 ? w - 1 : w;
+                int tu, lu;
+                double pu;
+                if (!b.out_edge(mid - 1, u, a, tu, lu, pu) || tu != w) continue;
+#pragma unroll
+                for (int o = 0; o < 3; ++o) {
+                    int tv, lv;
+                    double pv;
+                    if (!b.out_edge(mid, w, o, tv, lv, pv)) continue;
+                    const double prob = pu * pv;
+                    const int ml = lu ^ lv;
+                    int x = ml;
+                    if (dec) {
+                        if (ml != dj) continue;
+                        x = lv;
+                    }
+                    // new edge (u_layer_j, v_layer_j+1): j = 0 -> 0 -> tv; j = 1 -> u -> m
+                    if (j == 0) {
+                        c.vertex(tv);  // the from-vertex is the start (always present)
+                        c.template add<0>(tv * 2 + x, prob);
+                    } else {
+                        c.vertex(u);   // the to-vertex is the end (always present)
+                        c.template add<1>(u * 2 + x, prob);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// calcNormalizationVector + normalize of the depth-1 trellis (BinaryTrellis.py:280-306)
+PCUB_HD void n02_normalize(Child02& c) {
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < kN02E; ++i)
+        if (i < c.n0) {
+            if (c.k0[i] & 1) s1 += c.p0[i];
+            else s0 += c.p0[i];
+        }
+    double t = s0 >= s1 ? s0 : s1;
+    if (t == 0.0) t = 1.0;
+#pragma unroll
+    for (int i = 0; i < kN02E; ++i) c.p0[i] /= t;
+    s0 = 0.0;
+    s1 = 0.0;
+#pragma unroll
+    for (int wi = 0; wi < kN02V; ++wi) {
+        if (wi >= c.nw) continue;
+#pragma unroll
+        for (int i = 0; i < kN02E; ++i)
+            if (i < c.n1 && (c.k1[i] >> 1) == c.w[wi]) {
+                if (c.k1[i] & 1) s1 += c.p1[i];
+                else s0 += c.p1[i];
+            }
+    }
+    t = s0 >= s1 ? s0 : s1;
+    if (t == 0.0) t = 1.0;
+#pragma unroll
+    for (int i = 0; i < kN02E; ++i) c.p1[i] /= t;
+}
+
+// minus / plus (bit 0 of *dec) child of the depth-1 trellis collapsed to its
+// un-normalised marginal (trellis_collapse in trellis_body.h)
+PCUB_HD void n02_collapse(const Child02& c, const uint32_t* dec, double& m0, double& m1) {
+    m0 = 0.0;
+    m1 = 0.0;
+    const int dj = dec ? (int)(*dec & 1u) : 0;
+#pragma unroll
+    for (int wi = 0; wi < kN02V; ++wi) {
+        if (wi >= c.nw) continue;
+        const int w = c.w[wi];
+#pragma unroll
+        for (int a = 0; a < kN02E; ++a) {
+            if (a >= c.n0 || (c.k0[a] >> 1) != w) continue;
+#pragma unroll
+            for (int o = 0; o < kN02E; ++o) {
+                if (o >= c.n1 || (c.k1[o] >> 1) != w) continue;
+                const double prob = c.p0[a] * c.p1[o];
+                const int ml = (c.k0[a] ^ c.k1[o]) & 1;
+                int x = ml;
+                if (dec) {
+                    if (ml != dj) continue;
+                    x = c.k1[o] & 1;
+                }
+                if (x) m1 += prob;
+                else m0 += prob;
+            }
+        }
+    }
+}
+
+}  // namespace pcub

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "trellis_body.h"
+#include "trellis_n02.h"
 
 using namespace pcub;
 
@@ -111,6 +112,57 @@ struct Node {
     }
 };
 
+// n0 = 2 through the register-resident representation (trellis_n02.h), level-synchronous
+// over the T trellises: the kernel's del_n02 with XSub replaced by mem_sc.
+bool use_n02 = false;
+
+template <class BitF>
+std::vector<uint32_t> decode_n02(const BitF& bit, int len, int tb, double pd, Ctx& cx) {
+    const int T = 1 << tb;
+    std::vector<Base02> b(T);
+    for (int t = 0; t < T; ++t) {
+        int s, m;
+        segment_of(bit, len, tb, t, s, m);
+        b[t].m = m;
+        b[t].d = kN02L - m;
+        b[t].y = 0;
+        if (m <= kN02L)
+            for (int i = 0; i < m; ++i) b[t].y |= (uint32_t)(bit(s + i) & 1) << i;
+        b[t].pins = 0.5 * (1.0 - pd);
+        b[t].pdel = 0.5 * pd;
+    }
+    std::vector<Child02> c(T);
+    std::vector<uint32_t> y[2];
+    std::vector<double> vals(T);
+    for (int half = 0; half < 2; ++half) {
+        for (int t = 0; t < T; ++t) {
+            n02_transform(b[t], half ? &y[0][t] : nullptr, c[t]);
+            n02_normalize(c[t]);
+            double m0, m1;
+            n02_collapse(c[t], nullptr, m0, m1);
+            vals[t] = norm_pack(m0, m1);
+        }
+        const std::vector<int> xm = mem_sc(vals, cx);
+        for (int t = 0; t < T; ++t) {
+            double m0, m1;
+            const uint32_t d = (uint32_t)xm[t];
+            n02_collapse(c[t], &d, m0, m1);
+            vals[t] = norm_pack(m0, m1);
+        }
+        const std::vector<int> xp = mem_sc(vals, cx);
+        y[half].resize(T);
+        for (int t = 0; t < T; ++t) y[half][t] = (uint32_t)((xm[t] ^ xp[t]) | (xp[t] << 1));
+    }
+    std::vector<uint32_t> x(T);
+    for (int t = 0; t < T; ++t) {
+        const uint32_t ym = y[0][t], yp = y[1][t];
+        uint32_t o = 0;
+        for (int h = 0; h < 2; ++h) o |= ((((ym ^ yp) >> h) & 1u) << (2 * h)) | (((yp >> h) & 1u) << (2 * h + 1));
+        x[t] = o;
+    }
+    return x;
+}
+
 template <int N0>
 void decode_one(const uint8_t* w, int len, int n, double pd, Ctx& cx, std::vector<int>& xhat) {
     constexpr int L = 1 << N0;
@@ -123,7 +175,16 @@ void decode_one(const uint8_t* w, int len, int n, double pd, Ctx& cx, std::vecto
         segment_of(bit, len, tb, t, s, m);
         trellis_build<L>(base[t], bit, s, m, pd);
     }
-    const std::vector<uint32_t> x = Node<L, L>::run(base, cx);
+    std::vector<uint32_t> x;
+    if constexpr (N0 == 2) {
+        if (use_n02) {
+            x = decode_n02(bit, len, tb, pd, cx);
+        } else {
+            x = Node<L, L>::run(base, cx);
+        }
+    } else {
+        x = Node<L, L>::run(base, cx);
+    }
     xhat.assign((size_t)T * L, 0);
     for (int t = 0; t < T; ++t)
         for (int i = 0; i < L; ++i) xhat[(size_t)t * L + i] = (int)((x[t] >> i) & 1u);
@@ -160,3 +221,5 @@ extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, lon
     }
     return 0;
 }
+
+extern "C" void emu_set_n02(int on) { use_n02 = on != 0; }

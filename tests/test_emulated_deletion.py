@@ -40,7 +40,16 @@ def run(rx, rx_len, n, n0, pd, frozen, fval):
     return unpack_rows(info, K), unpack_rows(xh, N)
 
 
-def test_c5_golden():
+@pytest.fixture(params=[False, True], ids=["general", "n02"])
+def n02(request):
+    """Both trellis representations: the general one (trellis_body.h) and, for n0 = 2,
+    the register-resident one the kernel uses (trellis_n02.h)."""
+    emu().emu_set_n02(int(request.param))
+    yield request.param
+    emu().emu_set_n02(0)
+
+
+def test_c5_golden(n02):
     g = load_golden("deletion_n8")
     m = g["meta"]
     info, xhat = run(g["rx"], g["rx_len"], m["n"], m["n0"], m["pd"], g["frozen"], g["fval"])
@@ -49,7 +58,7 @@ def test_c5_golden():
 
 
 @pytest.mark.parametrize("idx", range(11))
-def test_edge_golden(idx):
+def test_edge_golden(idx, n02):
     c = deletion_edge_cases()[idx]
     n, n0, ones = (int(v) for v in c["shape"])
     if ones != 0 or n0 > 3:
@@ -57,3 +66,33 @@ def test_edge_golden(idx):
     info, xhat = run(c["rx"], c["rx_len"], n, n0, float(c["pd"][0]), c["frozen"], c["fval"])
     assert np.array_equal(info, c["info"])
     assert np.array_equal(xhat, c["xhat"])
+
+
+@pytest.mark.parametrize("n", [3, 5, 8])
+def test_n02_random_vs_oracle(n):
+    """Register-resident n0 = 2 path on random channel outputs and adversarial words."""
+    import random
+
+    from oracle import trellis_oracle as tro
+    emu().emu_set_n02(1)
+    try:
+        N = 1 << n
+        rng = np.random.default_rng(n)
+        prng = random.Random(n)
+        frozen = (rng.random(N) < 0.5).astype(np.uint8)
+        fval = (rng.random(N) < 0.5).astype(np.uint8)
+        words = []
+        for t in range(40):
+            x = [int(b) for b in rng.integers(0, 2, N)]
+            words.append(tro.deletion_channel(tro.add_guard_bands(x, n, 2, 0.1), [0.05, 0.2, 0.5][t % 3], prng))
+        words += [[], [1], [1, 1, 1, 1, 1], [int(b) for b in rng.integers(0, 2, 3 * N)]]
+        W = max(len(w) for w in words)
+        rx = np.zeros((len(words), W), np.uint8)
+        for i, w in enumerate(words):
+            rx[i, :len(w)] = w
+        info, xhat = run(rx, np.array([len(w) for w in words], np.int32), n, 2, 0.1, frozen, fval)
+        for i, w in enumerate(words):
+            xr, ir = tro.decode_deletion(w, n, 2, 0.1, frozen, fval)
+            assert list(info[i]) == ir and list(xhat[i]) == xr, i
+    finally:
+        emu().emu_set_n02(0)

@@ -636,6 +636,160 @@ def fx_main_deletion(R, timing):
     save("main_deletion_n8", dict(argv=argv[1:], lines=keep))
 
 
+def fx_test2(R, timing):
+    """The reference's test2.py itself (runpy): Tal-Vardy construction for BSC(0.11),
+    n=7, L=100, bound 0.1, then 4000 encode/decode trials.  Its channel draws from the
+    global `random` (unseeded in the script, test2.py:37); it is seeded with 7 here.
+    Records the stdout lines."""
+    import contextlib
+    import io
+    import runpy
+    buf = io.StringIO()
+    t0 = time.time()
+    random.seed(7)
+    with contextlib.redirect_stdout(buf):
+        runpy.run_path(os.path.join(REF, "test2.py"), run_name="__main__")
+    timing["test2_full_run_s"] = time.time() - t0
+    lines = buf.getvalue().strip().splitlines()
+    print("  reference test2:", lines[-1])
+    save("test2_run", dict(global_random_seed=7, lines=lines))
+
+
+def _construct_sources(R):
+    """Scalar channels for the construction fixtures (build-side choices)."""
+    BMD = R["BMD"]
+    rng = np.random.default_rng(2024)
+    out = {"bsc": BMD.makeBSC(0.11), "bec": BMD.makeBEC(0.3)}
+    rnd = BMD.BinaryMemorylessDistribution()
+    for _ in range(10):
+        a, b = rng.random(2)
+        rnd.append([float(a), float(b)])
+    rnd.append(list(rnd.probs[3]))                                  # exact duplicate letter
+    rnd.append([rnd.probs[5][0] * (1 + 3e-10), rnd.probs[5][1]])  # within math.isclose
+    rnd.append([0.0, 0.0])                                          # zero-probability letter
+    rnd.append([0.2, 0.2])                                          # LLR 0
+    out["random"] = rnd
+    awgn = BMD.BinaryMemorylessDistribution()                       # BI-AWGN quantised to 48 letters
+    s2 = 0.63
+    edges = np.linspace(-4, 4, 47)
+    grid = np.concatenate([[-np.inf], edges, [np.inf]])
+    from math import erf, sqrt
+
+    def cdf(v, m):
+        return 0.5 * (1 + erf((v - m) / sqrt(2 * s2))) if np.isfinite(v) else (0.0 if v < 0 else 1.0)
+    for lo, hi in zip(grid[:-1], grid[1:]):
+        awgn.append([0.5 * (cdf(hi, 1.0) - cdf(lo, 1.0)), 0.5 * (cdf(hi, -1.0) - cdf(lo, -1.0))])
+    out["awgn48"] = awgn
+    return out
+
+
+def fx_construct_bin(R, timing):
+    """Tal-Vardy construction (section 8(f) rank 3): the reference's own
+    mergeEquivalentSymbols / degrade / upgrade on several channels and their polar
+    transforms (auxiliary letter sets included), and calcFrozenSet_degradingUpgrading's
+    Pe vectors + frozen sets (TV = 0: the reference crashes with an x distribution)."""
+    import copy
+    BMD = R["BMD"]
+    arrays, cases = {}, []
+
+    def dist(pairs):
+        d = BMD.BinaryMemorylessDistribution()
+        for p in pairs:
+            d.append([float(p[0]), float(p[1])])
+        return d
+
+    for sname, src in _construct_sources(R).items():
+        variants = {"": src, "m": src.minusTransform(), "p": src.plusTransform()}
+        variants["pm"] = variants["m"].plusTransform() if len(src.probs) <= 4 else None
+        for vname, d0 in variants.items():
+            if d0 is None:
+                continue
+            case = sname + ("_" + vname if vname else "")
+            pairs = [list(p) for p in d0.probs]
+            arrays[case + "_in"] = np.array(pairs, np.float64)
+            d = dist(pairs)
+            d.auxiliary = [{i} for i in range(len(pairs))]
+            d.mergeEquivalentSymbols()
+            arrays[case + "_merged"] = np.array(d.probs, np.float64)
+            arrays[case + "_merged_aux"] = _aux_groups(d.auxiliary, len(pairs))
+            rec = {"case": case, "deg": [], "up": [], "up_err": []}
+            for L in (1, 2, 3, 8, 32):
+                d = dist(pairs)
+                d.auxiliary = [{i} for i in range(len(pairs))]
+                o = d.degrade(L)
+                arrays["%s_deg%d" % (case, L)] = np.array(o.probs, np.float64)
+                arrays["%s_deg%d_aux" % (case, L)] = _aux_groups(o.auxiliary, len(pairs))
+                rec["deg"].append(L)
+            for L in (1, 2, 3, 8, 32):
+                d = dist(pairs)
+                try:
+                    o = d.upgrade(L)
+                except Exception as e:  # the reference's own failure, recorded as expected
+                    rec["up_err"].append([L, type(e).__name__])
+                    continue
+                arrays["%s_up%d" % (case, L)] = np.array(o.probs, np.float64)
+                rec["up"].append(L)
+            cases.append(rec)
+    trees = []
+    for tname, n, L, bound, src in (("bsc_test2", 7, 100, 0.1, BMD.makeBSC(0.11)), ("bec", 6, 16, 0.05, BMD.makeBEC(0.4)),
+                                     ("random", 5, 8, 0.2, None)):
+        if src is None:
+            src = dist(_construct_sources(R)["random"].probs[:6])
+        pairs = [list(p) for p in src.probs]
+        t0 = time.time()
+        Pe = []
+        orig = R["BPED"].frozenSetFromTVAndPe
+
+        def capture(TV, Pe_, b, _orig=orig):
+            Pe.extend(Pe_)
+            return _orig(TV, Pe_, b)
+        R["BPED"].frozenSetFromTVAndPe = capture
+        try:
+            fz = BMD.calcFrozenSet_degradingUpgrading(n, L, bound, None, copy.deepcopy(src))
+        finally:
+            R["BPED"].frozenSetFromTVAndPe = orig
+        timing["construct_%s_n%d_L%d_s" % (tname, n, L)] = time.time() - t0
+        arrays[tname + "_tree_in"] = np.array(pairs, np.float64)
+        arrays[tname + "_tree_pe"] = np.array(Pe, np.float64)
+        mask = np.zeros(1 << n, np.uint8)
+        mask[sorted(fz)] = 1
+        arrays[tname + "_tree_frozen"] = mask
+        trees.append({"name": tname, "n": n, "L": L, "bound": bound})
+    # LinkedListHeap with tied keys: extraction order, neighbour key updates, final list
+    sys.path.insert(0, os.path.join(REF, "ScalarDistributions", "UpgradingDegrading"))
+    from ScalarDistributions.UpgradingDegrading import LinkedListHeap as LLH
+    hr = np.random.default_rng(11)
+    keys = hr.integers(0, 6, 40).astype(np.float64)
+    upd = hr.integers(0, 6, 2 * 30).astype(np.float64)
+    h = LLH.LinkedListHeap(list(keys), list(range(40)))
+    order, ui = [], 0
+    for _ in range(30):
+        e = h.extractHeapMin()
+        order.append(e.data)
+        for nb in (e.leftElementInList, e.rightElementInList):
+            if nb is not None:
+                h.updateKey(nb, float(upd[ui]))
+            ui += 1
+    arrays["heap_keys"] = keys
+    arrays["heap_updates"] = upd
+    arrays["heap_order"] = np.array(order, np.int64)
+    arrays["heap_final_list"] = np.array(h.returnData(), np.int64)
+    arrays["heap_final_array"] = np.array([el.data for el in h._heapArray], np.int64)
+    save("construct_bin", {"cases": cases, "trees": trees,
+                           "note": "reference BinaryMemorylessDistribution merge/degrade/upgrade/calcFrozenSet_degradingUpgrading"},
+         **arrays)
+
+
+def _aux_groups(aux, n):
+    """auxiliary (one set of input-letter indices per output letter) -> group[n], -1 = dropped"""
+    g = np.full(n, -1, np.int64)
+    for j, sset in enumerate(aux):
+        for i in sset:
+            assert g[i] == -1
+            g[i] = j
+    return g
+
+
 FIXTURES = {
     "bsc_n64": fx_bsc_n64,
     "awgn_n1024": lambda R, t: fx_awgn(R, t, 10, 64, 2.0, 20250204, "awgn_n1024", "C2"),
@@ -650,6 +804,8 @@ FIXTURES = {
     "deletion_edge": fx_deletion_edge,
     "genie_bsc_n64": fx_genie_bsc,
     "main_deletion_n8": fx_main_deletion,
+    "construct_bin": fx_construct_bin,
+    "test2_run": fx_test2,
 }
 
 

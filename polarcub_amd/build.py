@@ -3,7 +3,9 @@
     python -m polarcub_amd.build [--force]
 
 Compiles every csrc/*.hip translation unit to an object (in parallel, only the
-stale ones) and links polarcub_amd/lib/libpolarcub_hip.so with hipcc.
+stale ones) and links polarcub_amd/lib/libpolarcub_hip.so with hipcc; builds the
+host-only construction library polarcub_amd/lib/libpolarcub_construct.so
+(csrc/host/*.cpp) with g++.
 -ffp-contract=off is part of the arithmetic contract (no a*b+c contraction into
 FMA); never build with -ffast-math.
 """
@@ -25,6 +27,27 @@ SOURCES = ["sc_bin.hip", "sc_bin_k0.hip", "sc_bin_k1.hip", "sc_bin_k2.hip", "sc_
            "sc_util.hip", "sc_del.hip", "sc_leaf.hip", "sc_mc.hip"]
 CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-std=c++17", "-Wall",
           "-Wno-unused-function"]
+
+
+HOST_LIB = os.path.join(LIBDIR, "libpolarcub_construct.so")
+HOST_SOURCES = [os.path.join(CSRC, "host", "tv_construct.cpp")]
+CXX = os.environ.get("CXX", "g++")
+HOST_CFLAGS = ["-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-std=c++17", "-Wall", "-pthread"]
+
+
+def build_host(force=False, verbose=False):
+    """The construction library: plain C++, IEEE binary64 without contraction, libm log2."""
+    deps = HOST_SOURCES + [os.path.join(ROOT, "include", "polarcub_construct.h")]
+    if not force and not _stale(HOST_LIB, deps):
+        return HOST_LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    tmp = HOST_LIB + ".tmp"
+    cmd = [CXX] + HOST_CFLAGS + ["-I" + os.path.join(ROOT, "include")] + HOST_SOURCES + ["-o", tmp, "-lm"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, HOST_LIB)
+    return HOST_LIB
 
 
 def _headers():
@@ -64,6 +87,7 @@ def _compile(src, verbose):
 
 
 def build(force=False, verbose=False):
+    build_host(force, verbose)
     if not force and up_to_date():
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)

@@ -1,15 +1,103 @@
-"""Code construction helpers (host side, one-time per code).
+"""Code construction (host side, one-time per code).
 
-bhattacharyya_frozen follows the standard Bhattacharyya-parameter recursion for
-BI-AWGN in the reference's index convention (minus child = first half of the
-u range, BinaryPolarEncoderDecoder.py:289-317).  The reference's own
-degrading/upgrading construction (ScalarDistributions/BinaryMemorylessDistribution.py:624-680)
-is a separate, later component; frozen sets it produced are accepted as plain
-index sets everywhere.
+* The reference's Tal-Vardy degrading/upgrading construction
+  (ScalarDistributions/BinaryMemorylessDistribution.py:287-427, :624-680, with the
+  LinkedListHeap of ScalarDistributions/UpgradingDegrading/LinkedListHeap.py) runs in
+  the native host library libpolarcub_construct.so (csrc/host/tv_construct.cpp, C ABI
+  include/polarcub_construct.h), bit-identical to the reference, with the 2^m
+  channels of each tree level on a thread pool: merge_equivalent / degrade /
+  upgrade / tv_pe here, calcFrozenSet_degradingUpgrading in polarcub_amd.scalar.
+* bhattacharyya_frozen: the standard Bhattacharyya-parameter recursion for BI-AWGN
+  in the reference's index convention (minus child = first half of the u range,
+  BinaryPolarEncoderDecoder.py:289-317), used for the benchmark's code.
 """
+import ctypes
 import math
+import os
 
 import numpy as np
+
+_HOST = None
+
+# return codes of include/polarcub_construct.h -> the reference's exceptions
+_ERRORS = {-1: ValueError, -10: AssertionError, -11: ZeroDivisionError, -12: IndexError, -13: AttributeError}
+
+
+def host_lib():
+    """libpolarcub_construct.so (built by polarcub_amd.build / __graft_entry__.build)."""
+    global _HOST
+    if _HOST is None:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libpolarcub_construct.so")
+        if not os.path.exists(path):
+            raise RuntimeError("libpolarcub_construct.so not built: run `python -m polarcub_amd.build`")
+        lib = ctypes.CDLL(path)
+        P, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        lib.pcub_bmd_merge_equivalent.argtypes = [P, I64, P, P, P]
+        lib.pcub_bmd_degrade.argtypes = [P, I64, I64, P, P, P]
+        lib.pcub_bmd_upgrade.argtypes = [P, I64, I64, P, P]
+        lib.pcub_bin_construct.argtypes = [I32, I64, P, I64, P, I64, P, P, I32]
+        for f in (lib.pcub_bmd_merge_equivalent, lib.pcub_bmd_degrade, lib.pcub_bmd_upgrade, lib.pcub_bin_construct):
+            f.restype = ctypes.c_int
+        _HOST = lib
+    return _HOST
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise _ERRORS.get(rc, RuntimeError)("%s failed (code %d)" % (what, rc))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def _letters(probs):
+    a = np.ascontiguousarray(np.asarray(probs, dtype=np.float64).reshape(-1, 2))
+    return a
+
+
+def merge_equivalent(probs):
+    """mergeEquivalentSymbols on rows [p(y,0), p(y,1)] -> (merged rows, group) where
+    group[i] is the merged letter of input letter i (-1: zero probability, dropped)."""
+    a = _letters(probs)
+    out = np.empty_like(a)
+    grp = np.empty(len(a), np.int64)
+    n = ctypes.c_int64(0)
+    _check(host_lib().pcub_bmd_merge_equivalent(_ptr(a), len(a), _ptr(out), ctypes.byref(n), _ptr(grp)),
+           "mergeEquivalentSymbols")
+    return out[:n.value], grp
+
+
+def degrade(merged, L):
+    """degrade(L) of already-merged letters -> (letters, group of each merged letter)."""
+    a = _letters(merged)
+    out = np.empty_like(a)
+    grp = np.empty(len(a), np.int64)
+    n = ctypes.c_int64(0)
+    _check(host_lib().pcub_bmd_degrade(_ptr(a), len(a), int(L), _ptr(out), ctypes.byref(n), _ptr(grp)), "degrade")
+    return out[:n.value], grp
+
+
+def upgrade(merged, L):
+    """upgrade(L) of already-merged letters."""
+    a = _letters(merged)
+    out = np.empty_like(a)
+    n = ctypes.c_int64(0)
+    _check(host_lib().pcub_bmd_upgrade(_ptr(a), len(a), int(L), _ptr(out), ctypes.byref(n)), "upgrade")
+    return out[:n.value]
+
+
+def tv_pe(n, L, xprobs, xyprobs, threads=0):
+    """(TV, Pe) vectors of calcFrozenSet_degradingUpgrading: Pe of the degraded xy
+    channels, TV (total variation distance) of the upgraded x channels or zeros."""
+    xy = _letters(xyprobs)
+    x = None if xprobs is None else _letters(xprobs)
+    N = 1 << n
+    TV = np.empty(N)
+    Pe = np.empty(N)
+    _check(host_lib().pcub_bin_construct(int(n), int(L), _ptr(x), 0 if x is None else len(x), _ptr(xy), len(xy),
+                                         _ptr(TV), _ptr(Pe), int(threads)), "calcFrozenSet_degradingUpgrading")
+    return TV, Pe
 
 
 def awgn_sigma2(ebn0_db, rate):

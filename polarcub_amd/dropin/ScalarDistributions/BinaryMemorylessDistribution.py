@@ -1,2 +1,3 @@
-"""Drop-in alias of polarcub_amd.scalar (binary channels and factories)."""
-from polarcub_amd.scalar import BinaryMemorylessDistribution, eta, hxgiveny, makeBEC, makeBSC  # noqa: F401
+"""Drop-in alias of polarcub_amd.scalar (binary channels, factories, Tal-Vardy construction)."""
+from polarcub_amd.scalar import (BinaryMemorylessDistribution, calcFrozenSet_degradingUpgrading, eta,  # noqa: F401
+                                 eta_list, hxgiveny, makeBEC, makeBernoulli, makeBSC, naturalEta)

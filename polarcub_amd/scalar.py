@@ -7,23 +7,38 @@ hot path needs:
       calcXMarginal / calcYMarginal / probXGivenY               :429-443
       errorProb / bhattacharyya / totalVariationDistance / conditionalEntropy / mmse
       minusTransform / plusTransform (scalar channel transforms) :261-285
-  makeBSC(p) :485-490, makeBEC(p) :493-499
-The Tal-Vardy degrading/upgrading construction (:287-427, :624-680) is not part
-of the decode hot path; frozen sets it produced are accepted everywhere.
+      removeZeroProbOutput / sortProbs / mergeEquivalentSymbols  :92-208
+      degrade(L) / upgrade(L) (Tal-Vardy)                        :287-427
+  makeBSC(p) :485-490, makeBEC(p) :493-499, makeBernoulli(p) :502-506
+  calcFrozenSet_degradingUpgrading(n, L, bound, xDistribution, xyDistribution) :624-680
+  eta / eta_list / naturalEta / hxgiveny                        :450-477
+mergeEquivalentSymbols, degrade, upgrade and the construction run in the native
+host library (polarcub_amd.construction, csrc/host/tv_construct.cpp).
 """
 import math
+import sys
 
-from . import vectors
+from . import construction, vectors
 
 
 def eta(p):
-    assert 0 <= p <= 1
-    return 0.0 if p == 0 else -p * math.log2(p)
+    assert 0.0 <= p <= 1.0 + 10 * sys.float_info.epsilon
+    p = min(1.0, p)
+    return 0.0 if p == 0.0 else -p * math.log2(p)
+
+
+def eta_list(p_list):
+    return sum([eta(p) for p in p_list])
+
+
+def naturalEta(p):
+    assert 0.0 <= p <= 1.0
+    return 0.0 if p == 0.0 else -p * math.log(p)
 
 
 def hxgiveny(data):
-    s = data[0] + data[1]
-    return 0.0 if s == 0 else eta(data[0] / s) * s + eta(data[1] / s) * s
+    py = data[0] + data[1]
+    return py * (eta(data[0] / py) + eta(data[1] / py))
 
 
 class BinaryMemorylessDistribution:
@@ -107,6 +122,62 @@ class BinaryMemorylessDistribution:
                 out.append([y1[1] * y2[0], y1[0] * y2[1]])
         return out
 
+    # letter bookkeeping (the auxiliary list, when set, holds one set per letter)
+    def removeZeroProbOutput(self):
+        keep = [i for i, pair in enumerate(self.probs) if sum(pair) > 0.0]
+        self.probs = [self.probs[i] for i in keep]
+        if self.auxiliary is not None:
+            self.auxiliary = [self.auxiliary[i] for i in keep]
+
+    def sortProbs(self):
+        """Ascending p(x=0|y): letters with p(x=0|y) > 1/2 first (by p(x=1|y)), then the
+        rest (by -p(x=0|y)); stable, like the reference's list.sort."""
+        aux = self.auxiliary if self.auxiliary is not None else [None] * len(self.probs)
+        zero = [(p, a) for p, a in zip(self.probs, aux) if p[0] / sum(p) > 0.5]
+        one = [(p, a) for p, a in zip(self.probs, aux) if not p[0] / sum(p) > 0.5]
+        zero.sort(key=lambda t: t[0][1] / sum(t[0]))
+        one.sort(key=lambda t: -t[0][0] / sum(t[0]))
+        self.probs = [p for p, _ in zero + one]
+        if self.auxiliary is not None:
+            self.auxiliary = [a for _, a in zero + one]
+
+    def _merged_aux(self, group, count):
+        out = [set() for _ in range(count)]
+        for i, g in enumerate(group):
+            if g >= 0:
+                out[g] |= self.auxiliary[i]
+        return out
+
+    def mergeEquivalentSymbols(self):
+        """Merge letters whose posteriors are math.isclose, sort by LLR, normalise
+        (native, bit-identical).  Auxiliary sets are merged by union."""
+        merged, group = construction.merge_equivalent(self.probs)
+        if self.auxiliary is not None:
+            self.auxiliary = self._merged_aux(group, len(merged))
+        self.probs = merged.tolist()
+
+    def degrade(self, L):
+        """Degraded channel with at most L letters (greedy merge of LLR-adjacent letters
+        with the least mutual-information loss).  Merges self's equivalent letters first,
+        as the reference does; auxiliary sets are carried as unions."""
+        self.mergeEquivalentSymbols()
+        letters, group = construction.degrade(self.probs, L)
+        out = BinaryMemorylessDistribution()
+        out.probs = letters.tolist()
+        if self.auxiliary is not None:
+            out.auxiliary = self._merged_aux(group, len(letters))
+        return out
+
+    def upgrade(self, L):
+        """Upgraded channel with at most L letters (each removed letter's mass split onto
+        its neighbours).  Merges self's equivalent letters first."""
+        if self.auxiliary is not None:
+            raise NotImplementedError("upgrade with auxiliary letter sets")
+        self.mergeEquivalentSymbols()
+        out = BinaryMemorylessDistribution()
+        out.probs = construction.upgrade(self.probs, L).tolist()
+        return out
+
     def makeBinaryMemorylessVectorDistribution(self, length, yvec):
         vd = vectors.BinaryMemorylessVectorDistribution(length)
         if yvec is not None:
@@ -125,6 +196,27 @@ def makeBSC(p):
     bsc.append([0.5 * (1.0 - p), 0.5 * p])
     bsc.append([0.5 * p, 0.5 * (1.0 - p)])
     return bsc
+
+
+def makeBernoulli(p):
+    ber = BinaryMemorylessDistribution()
+    ber.append([1.0 - p, p])
+    return ber
+
+
+def calcFrozenSet_degradingUpgrading(n, L, upperBoundOnErrorProbability, xDistribution, xyDistribution, threads=0):
+    """Frozen set from the degraded xy tree (Pe) and the upgraded x tree (TV), at most L
+    letters per channel (ScalarDistributions/BinaryMemorylessDistribution.py:624-680).
+    The reference crashes for a non-None xDistribution (it calls a missing
+    totalVariation()); here TV is the upgraded channels' totalVariationDistance."""
+    from . import coding
+    assert n >= 0
+    assert L > 0
+    assert upperBoundOnErrorProbability > 0
+    assert xyDistribution is not None
+    TV, Pe = construction.tv_pe(n, L, None if xDistribution is None else xDistribution.probs, xyDistribution.probs,
+                                threads)
+    return coding.frozenSetFromTVAndPe(TV.tolist(), Pe.tolist(), upperBoundOnErrorProbability)
 
 
 def makeBEC(p):

@@ -8,9 +8,9 @@ import re
 from tests.conftest import ROOT
 
 
-def _declared():
+def _declared(header="*.h"):
     names = set()
-    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+    for h in glob.glob(os.path.join(ROOT, "include", header)):
         text = open(h).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         names.update(re.findall(r"\b(pcub_\w+)\s*\(", text))
@@ -28,9 +28,12 @@ def test_library_exports_every_declared_symbol():
     from polarcub_amd import _lib, build
     build.build()
     L = ctypes.CDLL(build.LIB)
-    missing = [n for n in sorted(_declared()) if not hasattr(L, n)]
+    missing = [n for n in sorted(_declared("polarcub_sc.h")) if not hasattr(L, n)]
     assert not missing, missing
-    assert set(_lib.EXPORTS) <= _declared()
+    assert set(_lib.EXPORTS) <= _declared("polarcub_sc.h")
+    H = ctypes.CDLL(build.HOST_LIB)  # host-only construction library (include/polarcub_construct.h)
+    missing = [n for n in sorted(_declared("polarcub_construct.h")) if not hasattr(H, n)]
+    assert not missing, missing
     assert _lib.lib().pcub_abi_version() == 1
 
 

@@ -107,6 +107,10 @@ def test_dropin_tree_imports():
         assert B.BinaryPolarEncoderDecoder is coding.BinaryPolarEncoderDecoder
         assert S.makeBSC is scalar.makeBSC
         assert V.BinaryMemorylessVectorDistribution is vectors.BinaryMemorylessVectorDistribution
+        assert S.calcFrozenSet_degradingUpgrading is scalar.calcFrozenSet_degradingUpgrading
+        from ScalarDistributions.UpgradingDegrading import LinkedListHeap as H
+        from polarcub_amd import heap
+        assert H.LinkedListHeap is heap.LinkedListHeap
     finally:
         sys.path.remove(d)
 

@@ -99,3 +99,14 @@ def test_main_deletion_cli_matches_reference_run():
     lines = [l for l in buf.getvalue().strip().splitlines()
              if not l.startswith(("TVVec", "pevec", "HEncvec", "HDecvec"))]
     assert lines == g["meta"]["lines"]
+
+
+def test_test2_cli_matches_reference_run():
+    """polarcub_amd.cli.test2 (native Tal-Vardy construction + 4000 GPU-batched trials)
+    with the reference run's channel seed prints the reference's lines, error count included."""
+    from polarcub_amd.cli import test2
+    g = load_golden("test2_run")
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        test2.main(["--seed", str(g["meta"]["global_random_seed"])])
+    assert buf.getvalue().strip().splitlines() == g["meta"]["lines"]

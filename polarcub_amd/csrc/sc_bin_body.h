@@ -351,23 +351,20 @@ PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
 }
 
 // Final pass into registers (F = 1 or 2): with F = 2, level D-1 is stored to
-// `l1`; level D (S values) goes into v.  Level D-1 is touched only here (as
-// l1, or as c.src when F = 1), which lets it live in LDS with static addressing.
+// lv[0]; level D (S values) goes into v.  Level D-1 is touched only by final
+// passes (stored here, or read as c.src when F = 1), which lets it live in LDS
+// with static addressing.  (A three-level final pass from the root needs more
+// than the 168 VGPRs of three waves/SIMD with S = 32 and spills.)
 template <int S, int F, bool FG, int R, int G, bool NS, bool LL>
-PCUB_HD void chain_final(const Chain& c, Lvl l1, double* v) {
+PCUB_HD void chain_final(const Chain& c, const Lvl* lv, double* v) {
     static_assert(F == 1 || F == 2, "final pass fuses at most two levels");
-    const Lvl lv[1] = {l1};
 #pragma unroll
     for (int p = 0; p < S; p += 2) {
         double2 y[(1 << F) - 1];
         colpair<F, FG, R, G, NS && F == 2, F == 2 || !LL>(c, p, S, y);
-        int off = 0;
+        if constexpr (F == 2) {
 #pragma unroll
-        for (int e = 1; e < F; ++e) {
-            const int He = 1 << (F - e);
-#pragma unroll
-            for (int m = 0; m < He; ++m) st2<false, !LL>(lv[e - 1].p + (long long)((p + m * S) >> 1) * lv[e - 1].s, y[off + m]);
-            off += He;
+            for (int m = 0; m < 2; ++m) st2<false, !LL>(lv[0].p + (long long)((p + m * S) >> 1) * lv[0].s, y[m]);
         }
         v[p] = y[(1 << F) - 2].x;
         v[p + 1] = y[(1 << F) - 2].y;
@@ -389,14 +386,26 @@ PCUB_HD void dispatch_pass(const Chain& c, int La, const LevelMap& lm, int a, bo
 }
 
 template <int S, int F, int G, int RR, bool NS, bool LL>
-PCUB_HD void dispatch_final(const Chain& c, Lvl l1, double* v, bool fg, bool root) {
+PCUB_HD void dispatch_final(const Chain& c, const Lvl* lv, double* v, bool fg, bool root) {
     if (root) {
-        if (fg) chain_final<S, F, true, RR, G, NS, LL>(c, l1, v);
-        else chain_final<S, F, false, RR, G, NS, LL>(c, l1, v);
+        if (fg) chain_final<S, F, true, RR, G, NS, LL>(c, lv, v);
+        else chain_final<S, F, false, RR, G, NS, LL>(c, lv, v);
     } else {
-        if (fg) chain_final<S, F, true, 0, G, NS, LL>(c, l1, v);
-        else chain_final<S, F, false, 0, G, NS, LL>(c, l1, v);
+        if (fg) chain_final<S, F, true, 0, G, NS, LL>(c, lv, v);
+        else chain_final<S, F, false, 0, G, NS, LL>(c, lv, v);
     }
+}
+
+// Split of a T-level chain into passes.  Each pass reads only its source level,
+// and levels halve at every depth, so passes are fused greedily from the top
+// (three levels each) and the final pass into registers (one or two levels)
+// takes the remainder: T = 3 -> 2 + 1, 4 -> 3 + 1, 5 -> 3 + 2, 6 -> 3 + 2 + 1.
+// With the deepest stage level in LDS (stored only by a final pass) the final
+// pass is two levels whenever T >= 2.
+template <bool LDS>
+PCUB_HD int final_levels(int T) {
+    if constexpr (LDS) return T >= 2 ? 2 : 1;
+    return (T % 3 == 2) ? 2 : 1;
 }
 
 // Decode codeword `cw` (clamped to a valid index for loads) with lane j of its
@@ -569,7 +578,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
             y = W::frozen(ub, fv, j) & SMASK;
         } else {
         int T = D - a;
-        const int Ffin = T >= 2 ? 2 : 1;
+        const int Ffin = final_levels<LDS>(T);
         while (T > Ffin) {
             const int F = (T - Ffin) >= 3 ? 3 : (T - Ffin);
             c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
@@ -586,12 +595,12 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         c.ystart = (k >> (D - a)) << (nv - a);
         if (Ffin == 2) {
             c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
-            dispatch_final<S, 2, G, RR, NS, LDS>(c, lastlv, v, fg, a == 0);
+            dispatch_final<S, 2, G, RR, NS, LDS>(c, &lastlv, v, fg, a == 0);
         } else if (a > 0) {
             c.src = lastlv;
-            dispatch_final<S, 1, G, RR, NS, LDS>(c, lastlv, v, fg, false);
+            dispatch_final<S, 1, G, RR, NS, LDS>(c, &lastlv, v, fg, false);
         } else {
-            dispatch_final<S, 1, G, RR, NS, LDS>(c, lastlv, v, fg, true);
+            dispatch_final<S, 1, G, RR, NS, LDS>(c, &lastlv, v, fg, true);
         }
         if (e0 == D) {  // the register subtree itself is rate-0 (its level-D values go unused)
             y = W::frozen(ub, fv, j) & SMASK;

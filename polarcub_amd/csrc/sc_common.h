@@ -74,8 +74,11 @@ PCUB_HD double op_f(double va, double vb) {
     const double p0 = 1.0 + m;
     const double p1 = a.r + b.r;
     const bool sw = p1 > p0;
-    const double num = sw ? p0 : p1;
-    const double den = sw ? p1 : p0;  // in [1, 2], or NaN
+    // p0 and p1 are both NaN (an input is the (0, 0) sentinel) or both numbers,
+    // so minNum/maxNum (v_min_f64 / v_max_f64) select exactly what the compare
+    // does; on a tie both are the same value.
+    const double num = __builtin_fmin(p0, p1);
+    const double den = __builtin_fmax(p0, p1);  // in [1, 2], or NaN
     return cv_pack(num / den, a.s ^ b.s ^ (sw ? 1u : 0u));
 }
 

@@ -73,9 +73,26 @@ PCUB_HD int first_frozen_depth(const uint32_t* fmask, int k, int D, int SU) {
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-PCUB_HD double xor_shfl(double v, int mask) { return __shfl_xor(v, mask); }
+// Exchange with lane ^ MASK.  Within a quad (MASK 1, 2) this is a DPP quad_perm
+// move (a VALU op, no LDS round trip: the cross-lane leaf chains are serial, so
+// the ds_bpermute latency is on the critical path); wider masks use __shfl_xor.
+// Every caller exchanges inside an aligned group of >= 2*MASK lanes that share
+// their control flow, so the source lane is always active.
+template <int MASK>
+PCUB_HD double xor_shfl_c(double v) {
+    if constexpr (MASK == 1 || MASK == 2) {
+        constexpr int ctrl = (MASK == 1) ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+        const unsigned long long b = (unsigned long long)as_bits(v);
+        const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, ctrl, 0xF, 0xF, false);
+        const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), ctrl, 0xF, 0xF, false);
+        return from_bits((long long)(((unsigned long long)hi << 32) | lo));
+    } else {
+        return __shfl_xor(v, MASK);
+    }
+}
 #else
-PCUB_HD double xor_shfl(double v, int) { return v; }  // host emulation runs G = 1 only
+template <int MASK>
+PCUB_HD double xor_shfl_c(double v) { return v; }  // host emulation runs G = 1 only
 #endif
 
 // A real node of length M (M <= G) with position (lane & (M-1)) held by each lane.
@@ -84,7 +101,7 @@ PCUB_HD double xor_shfl(double v, int) { return v; }  // host emulation runs G =
 template <int M, int UBASE>
 struct XSub {
     static PCUB_HD uint32_t run(double v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane) {
-        const double w = xor_shfl(v, M / 2);
+        const double w = xor_shfl_c<M / 2>(v);
         const bool lo = (lane & (M / 2)) == 0;
         const double a = lo ? v : w, b = lo ? w : v;
         if constexpr (M == 2) {

@@ -60,7 +60,7 @@ template <int M, int UBASE>
 struct XSubE {
     __device__ static uint32_t run(double v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane, double* leaf,
                                    long long B, bool store) {
-        const double w = xor_shfl(v, M / 2);
+        const double w = xor_shfl_c<M / 2>(v);
         const bool lo = (lane & (M / 2)) == 0;
         const double a = lo ? v : w, b = lo ? w : v;
         if constexpr (M == 2) {

@@ -131,7 +131,7 @@ long long qgrid(long long B, int q, int n) {
 size_t qslot_bytes(int n, int q) {
     const size_t N = (size_t)1 << n;
     const size_t S = (size_t)q_regs(q, n);
-    return (N - 2 * S) * q * sizeof(double) + N;
+    return (N - 2 * S) * (size_t)((q + 1) / 2) * sizeof(double2) + N;  // stage pairs + symbol words (N >= 4)
 }
 
 // rate-0 table + packed frozen words, ahead of the slots
@@ -179,8 +179,8 @@ extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, i
     A.xhat = xhat;
     A.nslots = g * kQBlock;
     char* slots = (char*)workspace + tb;
-    A.scratch = (double*)slots;
-    A.ysym = (uint8_t*)slots + (size_t)A.nslots * (N - 2 * S) * q * sizeof(double);
+    A.scratch = (double2*)slots;
+    A.ysym = (uint32_t*)(slots + (size_t)A.nslots * (N - 2 * S) * ((q + 1) / 2) * sizeof(double2));
     hipLaunchKernelGGL(qkernel(q, log2N), dim3((unsigned)g), dim3(kQBlock), 0, st, A);
     return (int)hipGetLastError();
 }

@@ -14,7 +14,9 @@
 // Schedule (as the binary kernel, sc_bin_body.h, with one codeword per lane):
 // half-split order inside every node; the bottom S positions of every chain live
 // in registers (QSub<S>); stage levels 1..D-1 in a per-slot scratch (q doubles
-// per position, slot-minor).  A chain -- one plus transform, then minus transforms
+// per position as ceil(q/2) 16-byte pairs, slot-minor, so a wave's access is one
+// contiguous 1 KiB); the re-encoded symbols one byte each, four to a 32-bit word
+// (combined word-wise, see q_combine_words).  A chain -- one plus transform, then minus transforms
 // down to depth D -- is evaluated in passes of up to two fused levels per column,
 // so a level written inside a pass is consumed from registers by the next one.
 // Nodes whose u range is entirely frozen are never evaluated (their symbols are 0
@@ -98,10 +100,31 @@ struct QArgs {
     const uint8_t* ef;      // [2^D] first rate-0 depth on each register subtree's chain
     uint8_t* info;          // [K][B]
     uint8_t* xhat;          // [N][B] or null
-    double* scratch;        // [(N - 2S) positions][Q][nslots]
-    uint8_t* ysym;          // [N][nslots]
+    double2* scratch;       // [(N - 2S) positions][ceil(Q/2)][nslots]
+    uint32_t* ysym;         // [N/4 words][nslots], symbol of position p in byte p % 4 of word p / 4
     long long nslots;
 };
+
+// Re-encoded symbols, four per word.  SWAR on bytes: every byte holds a value
+// < 2Q <= 16, so byte sums never carry, and (b | 0x80) - Q >= 0x78 never
+// borrows; its bit 7 is set iff b >= Q.
+template <int Q>
+PCUB_HD uint32_t q_mod_bytes(uint32_t s) {
+    const uint32_t ge = (((s | 0x80808080u) - (uint32_t)Q * 0x01010101u) & 0x80808080u) >> 7;
+    return s - ge * (uint32_t)Q;
+}
+
+// parent = [(ym + yp) % Q | (Q - yp) % Q]  (QaryPolarEncoderDecoder.py:397-399, half-split order)
+template <int Q>
+PCUB_HD void q_combine_words(uint32_t& m, uint32_t& p) {
+    const uint32_t mm = q_mod_bytes<Q>(m + p);
+    p = q_mod_bytes<Q>((uint32_t)Q * 0x01010101u - p);
+    m = mm;
+}
+
+PCUB_HD int q_sym(const uint32_t* Y, long long ns, int pos) {
+    return (int)((Y[(long long)(pos >> 2) * ns] >> ((pos & 3) * 8)) & 0xffu);
+}
 
 // Decisions of the register subtree: information symbols go out in u order.
 struct QInfo {
@@ -153,10 +176,26 @@ PCUB_HD QV<Q> q_load(const double* base, long long pos, long long stride) {
     return v;
 }
 
+// stage levels: position pos as QP = ceil(Q/2) pairs (an odd Q pads the last one)
 template <int Q>
-PCUB_HD void q_store(double* base, long long pos, long long stride, const QV<Q>& v) {
+PCUB_HD QV<Q> q_load2(const double2* base, long long pos, long long stride) {
+    constexpr int QP = (Q + 1) / 2;
+    QV<Q> v;
 #pragma unroll
-    for (int x = 0; x < Q; ++x) base[(pos * Q + x) * stride] = v.p[x];
+    for (int h = 0; h < QP; ++h) {
+        const double2 d = ld2(base + (pos * QP + h) * stride);
+        v.p[2 * h] = d.x;
+        if (2 * h + 1 < Q) v.p[2 * h + 1] = d.y;
+    }
+    return v;
+}
+
+template <int Q>
+PCUB_HD void q_store2(double2* base, long long pos, long long stride, const QV<Q>& v) {
+    constexpr int QP = (Q + 1) / 2;
+#pragma unroll
+    for (int h = 0; h < QP; ++h)
+        st2(base + (pos * QP + h) * stride, double2{v.p[2 * h], (2 * h + 1 < Q) ? v.p[2 * h + 1] : 0.0});
 }
 
 // Value at position p of the depth-a node on the current chain: the raw root for
@@ -165,13 +204,13 @@ struct QLev {
     const double* in;   // root: row i, symbol x at in[(i * B) * Q + x]
     long long B;
     int n;
-    const double* scr;
+    const double2* scr;
     long long ns;
     int N;
     template <int Q>
     PCUB_HD QV<Q> get(int a, int p) const {
         if (a == 0) return q_load<Q>(in, (long long)bitrev((uint32_t)p, n) * B, 1);
-        return q_load<Q>(scr, (long long)N - 2 * (N >> a) + p, ns);
+        return q_load2<Q>(scr, (long long)N - 2 * (N >> a) + p, ns);
     }
 };
 
@@ -183,8 +222,8 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
     const int N = 1 << n;
     const long long ns = A.nslots;
     const int D = n - s;  // depth of the register nodes
-    double* scr = A.scratch + slot;
-    uint8_t* Y = A.ysym + slot;
+    double2* scr = A.scratch + slot;
+    uint32_t* Y = A.ysym + slot;
     QLev lv{A.xy + cw * Q, A.B, n, scr, ns, N};
     QInfo qi{&A, cw, store, 0};
     for (int k = 0; k < (1 << D); ++k) {
@@ -206,17 +245,17 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
 #pragma unroll
                     for (int m = 0; m < 2; ++m) {
                         const QV<Q> x0 = lv.template get<Q>(a, p + m * C), x1 = lv.template get<Q>(a, p + (m + 2) * C);
-                        l1[m] = gop ? q_plus<Q>(x0, x1, Y[(long long)(ystart + p + m * C) * ns]) : q_minus<Q>(x0, x1);
-                        q_store<Q>(scr, (long long)N - 2 * (N >> (a + 1)) + p + m * C, ns, l1[m]);
+                        l1[m] = gop ? q_plus<Q>(x0, x1, q_sym(Y, ns, ystart + p + m * C)) : q_minus<Q>(x0, x1);
+                        q_store2<Q>(scr, (long long)N - 2 * (N >> (a + 1)) + p + m * C, ns, l1[m]);
                     }
-                    q_store<Q>(scr, (long long)N - 2 * (N >> (a + 2)) + p, ns, q_minus<Q>(l1[0], l1[1]));
+                    q_store2<Q>(scr, (long long)N - 2 * (N >> (a + 2)) + p, ns, q_minus<Q>(l1[0], l1[1]));
                 }
             } else {
                 const int C = La >> 1;
                 for (int p = 0; p < C; ++p) {
                     const QV<Q> x0 = lv.template get<Q>(a, p), x1 = lv.template get<Q>(a, p + C);
-                    const QV<Q> o = gop ? q_plus<Q>(x0, x1, Y[(long long)(ystart + p) * ns]) : q_minus<Q>(x0, x1);
-                    q_store<Q>(scr, (long long)N - 2 * (N >> (a + 1)) + p, ns, o);
+                    const QV<Q> o = gop ? q_plus<Q>(x0, x1, q_sym(Y, ns, ystart + p)) : q_minus<Q>(x0, x1);
+                    q_store2<Q>(scr, (long long)N - 2 * (N >> (a + 1)) + p, ns, o);
                 }
             }
             a += F;
@@ -230,28 +269,52 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
 #pragma unroll
             for (int p = 0; p < S; ++p) {
                 const QV<Q> x0 = lv.template get<Q>(a, p), x1 = lv.template get<Q>(a, p + S);
-                v[p] = gop ? q_plus<Q>(x0, x1, Y[(long long)(ystart + p) * ns]) : q_minus<Q>(x0, x1);
+                v[p] = gop ? q_plus<Q>(x0, x1, q_sym(Y, ns, ystart + p)) : q_minus<Q>(x0, x1);
             }
             QSub<Q, S>::run(v, y, k * S, qi);
         } else {
 #pragma unroll
             for (int j = 0; j < S; ++j) y[j] = 0;  // rate-0: symbols 0, re-encoding 0
         }
+        // the subtree's symbols into its words (S < 4: a part of one word)
+        if constexpr (S >= 4) {
 #pragma unroll
-        for (int j = 0; j < S; ++j) Y[(long long)(k * S + j) * ns] = y[j];
+            for (int w = 0; w < S / 4; ++w)
+                Y[(long long)(k * S / 4 + w) * ns] = (uint32_t)y[4 * w] | ((uint32_t)y[4 * w + 1] << 8) |
+                                                     ((uint32_t)y[4 * w + 2] << 16) | ((uint32_t)y[4 * w + 3] << 24);
+        } else {
+            uint32_t* yw = Y + (long long)((k * S) >> 2) * ns;
+            const int sh = ((k * S) & 3) * 8;
+            uint32_t ws = 0;
+#pragma unroll
+            for (int j = 0; j < S; ++j) ws |= (uint32_t)y[j] << (8 * j);
+            *yw = (sh == 0 ? 0u : (*yw & ((1u << sh) - 1u))) | (ws << sh);
+        }
         // combine completed plus children: [(ym+yp)%q | (q-yp)%q]
         for (int d = D; d >= 1 && ((k >> (D - d)) & 1); --d) {
             const int Lc = N >> d;
             const long long st = (long long)(k >> (D - d + 1)) * 2 * Lc;
-            for (int p = 0; p < Lc; ++p) {
-                const int ym = Y[(st + p) * ns], yp = Y[(st + Lc + p) * ns];
-                Y[(st + p) * ns] = (uint8_t)((ym + yp) % Q);
-                Y[(st + Lc + p) * ns] = (uint8_t)((Q - yp) % Q);
+            if (Lc >= 4) {
+                for (int w = 0; w < Lc / 4; ++w) {
+                    uint32_t* pm = Y + (st / 4 + w) * ns;
+                    uint32_t* pp = Y + (st / 4 + Lc / 4 + w) * ns;
+                    uint32_t m = *pm, p = *pp;
+                    q_combine_words<Q>(m, p);
+                    *pm = m;
+                    *pp = p;
+                }
+            } else {  // Lc = 1, 2: the parent is 2 or 4 bytes of one word
+                uint32_t* pw = Y + (st >> 2) * ns;
+                const int sh = (int)(st & 3) * 8;
+                const uint32_t lm = (Lc == 1) ? 0xffu : 0xffffu;
+                uint32_t m = (*pw >> sh) & lm, p = (*pw >> (sh + 8 * Lc)) & lm;
+                q_combine_words<Q>(m, p);
+                *pw = (*pw & ~(((lm << (8 * Lc)) | lm) << sh)) | (((p << (8 * Lc)) | m) << sh);
             }
         }
     }
     if (A.xhat && store)
-        for (int i = 0; i < N; ++i) A.xhat[(long long)i * A.B + cw] = Y[(long long)bitrev((uint32_t)i, n) * ns];
+        for (int i = 0; i < N; ++i) A.xhat[(long long)i * A.B + cw] = (uint8_t)q_sym(Y, ns, (int)bitrev((uint32_t)i, n));
 }
 
 }  // namespace pcub

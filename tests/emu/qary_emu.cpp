@@ -19,8 +19,8 @@ static int run(const double* xy, long long B, int n, const uint8_t* frozen, uint
     const int D = n - s;
     std::vector<uint8_t> ef((size_t)1 << D);
     for (int k = 0; k < (1 << D); ++k) ef[k] = (uint8_t)first_frozen_depth(words.data(), k, D, S);
-    std::vector<double> scr((size_t)(N - 2 * S) * Q * ns + 1);
-    std::vector<uint8_t> ys((size_t)N * ns);
+    std::vector<double2> scr((size_t)(N - 2 * S) * ((Q + 1) / 2) * ns + 1);
+    std::vector<uint32_t> ys((size_t)(N + 3) / 4 * ns);
     QArgs A;
     A.xy = xy;
     A.B = B;

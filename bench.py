@@ -304,6 +304,8 @@ def main():
     ap.add_argument("--seed", type=int, default=20250204)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-xhat", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end Monte-Carlo leg (profiling: only the timed decode launches)")
     a = ap.parse_args()
 
     world, rank, local = mc.dist_env()
@@ -344,7 +346,7 @@ def main():
     total_cw = counters[0] * a.steps
     value = total_cw / elapsed
     e2e = None
-    if hasattr(w, "end_to_end"):
+    if hasattr(w, "end_to_end") and not a.no_e2e:
         if world > 1:
             dist.barrier()
         _, e2e_s = mc.reduce_counters([0], w.end_to_end(), device if world > 1 else None)

@@ -23,7 +23,7 @@ if [ -z "${NO_BENCH:-}" ]; then
 fi
 if [ -n "${PROF:-}" ]; then
   cd /tmp
-  timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --batch $BATCH --no-cpu ${BENCH_EXTRA:-} > $R/gpurun_out/prof.log 2>&1
+  timeout -k 10 ${T_PROF:-400} rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --batch $BATCH --no-cpu --no-e2e ${BENCH_EXTRA:-} > $R/gpurun_out/prof.log 2>&1
   rc=$?; echo "prof rc=$rc"; tail -2 $R/gpurun_out/prof.log
   cd $R
   [ $rc -eq 0 ] || exit $rc

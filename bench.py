@@ -235,6 +235,8 @@ class Qary:
         mask = np.ones(self.N, np.uint8)
         mask[order[:self.K]] = 0
         self.code = sc.QaryCode(self.q, self.N, mask, device=device)
+        if a.qlanes:
+            sc.set_qary_lanes(a.qlanes)
         self.dec = sc.QaryDecoder(self.code)
         gen = torch.Generator(device=device)
         gen.manual_seed(mc.shard_seed(a.seed, rank))
@@ -298,6 +300,7 @@ def main():
     ap.add_argument("--xi", type=float, default=0.1, help="guard-band parameter")
     ap.add_argument("--q", type=int, default=4)
     ap.add_argument("--qsc-p", type=float, default=0.11)
+    ap.add_argument("--qlanes", type=int, default=0, help="q-ary: lanes per codeword (0 = the library's)")
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU")
     ap.add_argument("--variant", type=int, default=None, help="binary decode kernel variant (default: the library's)")
     ap.add_argument("--max-blocks", type=int, default=0, help="cap decode workgroups per CU (0 = occupancy)")

@@ -11,9 +11,10 @@
 //   frozen symbols are 0 (:347-351); the a-priori tree is never consulted.
 //   combine x[2h] = (xm+xp)%q, x[2h+1] = (q-xp)%q                                    (:397-399)
 // The per-codeword schedule (register subtrees, fused chain passes, rate-0
-// skipping) is in sc_qary_body.h; this file owns the launch geometry: one
-// codeword per lane, 256-thread workgroups, a resident grid striding over
-// 256-codeword tiles so the per-slot stage buffers are reused.
+// skipping, G lanes per codeword) is in sc_qary_body.h; this file owns the
+// launch geometry: G lanes per codeword (default 2, fewer for short codes),
+// 256-thread workgroups, a resident grid striding over 256/G-codeword tiles so
+// the per-slot stage buffers are reused.
 #include <hip/hip_runtime.h>
 
 #include "polarcub_sc.h"
@@ -26,14 +27,17 @@ namespace {
 constexpr int kQBlock = 256;
 constexpr int kQWaves = 3;  // waves per SIMD the register allocation must allow (3 workgroups per CU)
 
-template <int Q, int S>
+template <int Q, int S, int G>
 __global__ __launch_bounds__(kQBlock, kQWaves) void k_sc_qary(QArgs A) {
+    constexpr int CWB = kQBlock / G;  // codewords per tile
     const long long slot = (long long)blockIdx.x * kQBlock + threadIdx.x;
-    const long long ntiles = (A.B + kQBlock - 1) / kQBlock;
+    const int j = threadIdx.x & (G - 1);
+    const int lane = threadIdx.x & 63;
+    const long long ntiles = (A.B + CWB - 1) / CWB;
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const long long cw = t * kQBlock + threadIdx.x;
+        const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_qary_cw<Q, S>(A, valid ? cw : A.B - 1, slot, valid);
+        decode_qary_cw<Q, S, G>(A, valid ? cw : A.B - 1, slot, valid, j, lane);
     }
 }
 
@@ -81,36 +85,53 @@ __global__ __launch_bounds__(kQBlock) void k_encode_qary(const uint8_t* info, lo
 
 typedef void (*QKern)(QArgs);
 
-// register positions per chain: 8 for q <= 4, 4 for q <= 8, at most N/2
-int q_regs(int q, int n) {
-    int S = q <= 4 ? 8 : 4;
-    while (S > 1 && (1 << n) < 2 * S) S >>= 1;
-    return S;
+int g_qlanes = 2;  // requested lanes per codeword (pcub_sc_set_qary_lanes): 2 is the fastest at q=4 N=256
+
+// register positions per lane S and lanes per codeword G for a code of 2^n:
+// S = 8 (q <= 4) or 4, G = the requested lanes, both reduced until N >= 2*S*G
+struct QGeom {
+    int S, G;
+};
+QGeom q_geom(int q, int n) {
+    QGeom c{q <= 4 ? 8 : 4, g_qlanes};
+    while (c.G > 1 && (1 << n) < 2 * c.S * c.G) c.G >>= 1;
+    while (c.S > 1 && (1 << n) < 2 * c.S * c.G) c.S >>= 1;
+    return c;
 }
 
-template <int Q>
+template <int Q, int G>
 QKern qkernel_s(int S) {
     switch (S) {
-        case 1: return k_sc_qary<Q, 1>;
-        case 2: return k_sc_qary<Q, 2>;
-        case 4: return k_sc_qary<Q, 4>;
+        case 1: return k_sc_qary<Q, 1, G>;
+        case 2: return k_sc_qary<Q, 2, G>;
+        case 4: return k_sc_qary<Q, 4, G>;
         case 8:
-            if constexpr (Q <= 4) return k_sc_qary<Q, 8>;
+            if constexpr (Q <= 4) return k_sc_qary<Q, 8, G>;
             else return nullptr;
         default: return nullptr;
     }
 }
 
+template <int Q>
+QKern qkernel_g(QGeom c) {
+    switch (c.G) {
+        case 1: return qkernel_s<Q, 1>(c.S);
+        case 2: return qkernel_s<Q, 2>(c.S);
+        case 4: return qkernel_s<Q, 4>(c.S);
+        default: return nullptr;
+    }
+}
+
 QKern qkernel(int q, int n) {
-    const int S = q_regs(q, n);
+    const QGeom c = q_geom(q, n);
     switch (q) {
-        case 2: return qkernel_s<2>(S);
-        case 3: return qkernel_s<3>(S);
-        case 4: return qkernel_s<4>(S);
-        case 5: return qkernel_s<5>(S);
-        case 6: return qkernel_s<6>(S);
-        case 7: return qkernel_s<7>(S);
-        case 8: return qkernel_s<8>(S);
+        case 2: return qkernel_g<2>(c);
+        case 3: return qkernel_g<3>(c);
+        case 4: return qkernel_g<4>(c);
+        case 5: return qkernel_g<5>(c);
+        case 6: return qkernel_g<6>(c);
+        case 7: return qkernel_g<7>(c);
+        case 8: return qkernel_g<8>(c);
         default: return nullptr;
     }
 }
@@ -123,20 +144,27 @@ long long qgrid(long long B, int q, int n) {
     // the launch bounds guarantee kQWaves resident workgroups per CU (the occupancy
     // query reports 1 for these kernels on ROCm 7.2)
     if (occ < kQWaves) occ = kQWaves;
-    const long long ntiles = (B + kQBlock - 1) / kQBlock;
+    const long long cwb = kQBlock / q_geom(q, n).G;
+    const long long ntiles = (B + cwb - 1) / cwb;
     const long long g = (long long)cus * occ;
     return ntiles < g ? ntiles : g;
 }
 
+// per lane: virtual stage levels 1..D-1 (Nv - 2S positions as pairs) + Nv symbol bytes in words
 size_t qslot_bytes(int n, int q) {
-    const size_t N = (size_t)1 << n;
-    const size_t S = (size_t)q_regs(q, n);
-    return (N - 2 * S) * (size_t)((q + 1) / 2) * sizeof(double2) + N;  // stage pairs + symbol words (N >= 4)
+    const QGeom c = q_geom(q, n);
+    const size_t Nv = ((size_t)1 << n) / c.G;
+    return (Nv - 2 * c.S) * (size_t)((q + 1) / 2) * sizeof(double2) + ((Nv + 3) & ~(size_t)3);
+}
+
+int q_depth(int n, int q) {
+    const QGeom c = q_geom(q, n);
+    return n - __builtin_ctz((unsigned)(c.S * c.G));
 }
 
 // rate-0 table + packed frozen words, ahead of the slots
 size_t qtable_bytes(int n, int q) {
-    const int D = n - __builtin_ctz((unsigned)q_regs(q, n));
+    const int D = q_depth(n, q);
     return ((((size_t)1 << n) + 31) / 32 * 4 + ((size_t)1 << D) + 255) & ~(size_t)255;
 }
 
@@ -160,15 +188,15 @@ extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, i
     if (!workspace || workspace_bytes < tb + per_block) return PCUB_EINVAL;
     if ((size_t)g * per_block > workspace_bytes - tb) g = (long long)((workspace_bytes - tb) / per_block);
     const int N = 1 << log2N;
-    const int S = q_regs(q, log2N);
-    const int D = log2N - __builtin_ctz((unsigned)S);
+    const QGeom c = q_geom(q, log2N);
+    const int D = q_depth(log2N, q);
     hipStream_t st = (hipStream_t)stream;
     uint32_t* words = (uint32_t*)workspace;
     uint8_t* ef = (uint8_t*)workspace + ((size_t)N + 31) / 32 * 4;
     hipLaunchKernelGGL(k_q_frozen_words, dim3((unsigned)(((N + 31) / 32 + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0, st,
                        frozen, N, words);
-    hipLaunchKernelGGL(k_q_ef, dim3((unsigned)(((1 << D) + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0, st, words, D, S,
-                       ef);
+    hipLaunchKernelGGL(k_q_ef, dim3((unsigned)(((1 << D) + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0, st, words, D,
+                       c.S * c.G, ef);
     QArgs A;
     A.xy = xy;
     A.B = B;
@@ -180,7 +208,7 @@ extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, i
     A.nslots = g * kQBlock;
     char* slots = (char*)workspace + tb;
     A.scratch = (double2*)slots;
-    A.ysym = (uint32_t*)(slots + (size_t)A.nslots * (N - 2 * S) * ((q + 1) / 2) * sizeof(double2));
+    A.ysym = (uint32_t*)(slots + (size_t)A.nslots * (N / c.G - 2 * c.S) * ((q + 1) / 2) * sizeof(double2));
     hipLaunchKernelGGL(qkernel(q, log2N), dim3((unsigned)g), dim3(kQBlock), 0, st, A);
     return (int)hipGetLastError();
 }
@@ -193,4 +221,13 @@ extern "C" int pcub_polar_encode_qary(const uint8_t* info, int64_t B, int32_t lo
     hipLaunchKernelGGL(k_encode_qary, dim3((unsigned)((B + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0,
                        (hipStream_t)stream, info, (long long)B, log2N, q, frozen, x);
     return (int)hipGetLastError();
+}
+
+// Tuning hook (not part of the stable ABI): lanes per codeword of the q-ary
+// decode kernel (1, 2 or 4; reduced for short codes).  Returns the previous value.
+extern "C" int pcub_sc_set_qary_lanes(int G) {
+    if (G != 1 && G != 2 && G != 4) return PCUB_EINVAL;
+    const int old = g_qlanes;
+    g_qlanes = G;
+    return old;
 }

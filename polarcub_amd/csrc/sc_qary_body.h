@@ -21,6 +21,13 @@
 // so a level written inside a pass is consumed from registers by the next one.
 // Nodes whose u range is entirely frozen are never evaluated (their symbols are 0
 // and so is their re-encoding), driven by the per-code rate-0 depth table `ef`.
+//
+// G lanes per codeword (G = 1, 2, 4), as in the binary kernel: lane j owns the
+// positions p = j (mod G) of every node of length >= G, so every butterfly of a
+// node of length >= 2G is lane-local and each lane runs the G = 1 schedule on a
+// virtual tree of N/G positions; a virtual leaf is a real node of G positions,
+// one per lane, finished by QXSub<G> with cross-lane exchanges.  More lanes per
+// codeword = fewer stage levels in memory (the kernel is bound by their traffic).
 #pragma once
 #include "sc_bin_body.h"  // first_frozen_depth, launder
 #include "sc_common.h"
@@ -126,25 +133,73 @@ PCUB_HD int q_sym(const uint32_t* Y, long long ns, int pos) {
     return (int)((Y[(long long)(pos >> 2) * ns] >> ((pos & 3) * 8)) & 0xffu);
 }
 
-// Decisions of the register subtree: information symbols go out in u order.
+// Decisions of the register subtree: information symbols go out in u order
+// (identical in the G lanes of a codeword; lane w % G stores row w).
 struct QInfo {
     const QArgs* A;
     long long cw;
     bool store;
-    int w;  // next information row
+    int w;     // next information row
+    int j;     // lane of the codeword
+    int gm;    // G - 1
     PCUB_HD void put(int u) {
-        if (store) A->info[(long long)w * A->B + cw] = (uint8_t)u;
+        if (store && (w & gm) == j) A->info[(long long)w * A->B + cw] = (uint8_t)u;
         ++w;
     }
 };
 
-// Register-resident node of L positions (half-split); leaf u indices UB .. UB+L-1.
-template <int Q, int L>
-struct QSub {
-    static PCUB_HD void run(const QV<Q>* v, uint8_t* y, int ub, QInfo& qi) {
-        if constexpr (L == 1) {
-            int u = 0;
+// Exchange of a whole q-vector with lane ^ MASK.
+template <int Q, int MASK>
+PCUB_HD QV<Q> q_shfl(const QV<Q>& v) {
+    QV<Q> w;
+#pragma unroll
+    for (int x = 0; x < Q; ++x) w.p[x] = xor_shfl_c<MASK>(v.p[x]);
+    return w;
+}
+
+// A real node of M <= G positions, position (lane & (M-1)) in each lane; leaf u
+// indices UB .. UB+M-1.  Returns this lane's symbol of the node's re-encoding.
+template <int Q, int M>
+struct QXSub {
+    static PCUB_HD int run(const QV<Q>& v, int ub, QInfo& qi, int lane) {
+        const QV<Q> w = q_shfl<Q, M / 2>(v);
+        const bool lo = (lane & (M / 2)) == 0;
+        QV<Q> a, b;
+#pragma unroll
+        for (int x = 0; x < Q; ++x) {
+            a.p[x] = lo ? v.p[x] : w.p[x];
+            b.p[x] = lo ? w.p[x] : v.p[x];
+        }
+        int ym, yp;
+        if constexpr (M == 2) {
+            ym = 0;
             if (!qi.A->frozen[ub]) {
+                ym = q_leaf<Q>(q_minus<Q>(a, b));
+                qi.put(ym);
+            }
+            yp = 0;
+            if (!qi.A->frozen[ub + 1]) {
+                yp = q_leaf<Q>(q_plus<Q>(a, b, ym));
+                qi.put(yp);
+            }
+        } else {
+            ym = QXSub<Q, M / 2>::run(q_minus<Q>(a, b), ub, qi, lane);
+            yp = QXSub<Q, M / 2>::run(q_plus<Q>(a, b, ym), ub + M / 2, qi, lane);
+        }
+        return lo ? (ym + yp) % Q : (Q - yp) % Q;
+    }
+};
+
+// Register-resident node of L virtual positions (half-split); virtual leaves
+// VB .. VB+L-1, i.e. real u indices VB*G .. (VB+L)*G - 1.
+template <int Q, int L, int G>
+struct QSub {
+    static PCUB_HD void run(const QV<Q>* v, uint8_t* y, int vb, QInfo& qi, int lane) {
+        if constexpr (L == 1 && G > 1) {
+            y[0] = (uint8_t)QXSub<Q, G>::run(v[0], vb * G, qi, lane);
+        } else if constexpr (L == 1) {
+            int u = 0;
+            if (!qi.A->frozen[vb]) {
                 u = q_leaf<Q>(v[0]);
                 qi.put(u);
             }
@@ -155,10 +210,10 @@ struct QSub {
             uint8_t ym[H], yp[H];
 #pragma unroll
             for (int j = 0; j < H; ++j) c[j] = q_minus<Q>(v[j], v[j + H]);
-            QSub<Q, H>::run(c, ym, ub, qi);
+            QSub<Q, H, G>::run(c, ym, vb, qi, lane);
 #pragma unroll
             for (int j = 0; j < H; ++j) c[j] = q_plus<Q>(v[j], v[j + H], ym[j]);
-            QSub<Q, H>::run(c, yp, ub + H, qi);
+            QSub<Q, H, G>::run(c, yp, vb + H, qi, lane);
 #pragma unroll
             for (int j = 0; j < H; ++j) {
                 y[j] = (uint8_t)((ym[j] + yp[j]) % Q);
@@ -214,18 +269,23 @@ struct QLev {
     }
 };
 
-// S = register positions (a power of two, N >= 2S).
-template <int Q, int S>
-PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store) {
+// S = register positions per lane (a power of two), G lanes per codeword
+// (lane j of them, `lane` = wave lane id); requires N >= 2*S*G.  Below, n and N
+// are the virtual (per-lane) tree: n = log2(N_real / G).
+template <int Q, int S, int G = 1>
+PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store, int j = 0, int lane = 0) {
     constexpr int s = (S == 1) ? 0 : (S == 2) ? 1 : (S == 4) ? 2 : (S == 8) ? 3 : 4;
-    const int n = A.n;
+    constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : 2;
+    static_assert(G == 1 || G == 2 || G == 4, "lanes per codeword");
+    const int n = A.n - g;
     const int N = 1 << n;
     const long long ns = A.nslots;
     const int D = n - s;  // depth of the register nodes
     double2* scr = A.scratch + slot;
     uint32_t* Y = A.ysym + slot;
-    QLev lv{A.xy + cw * Q, A.B, n, scr, ns, N};
-    QInfo qi{&A, cw, store, 0};
+    // root rows of lane j: real position j + G*t is row bitrev_n(j) + bitrev_{n-g}(t)
+    QLev lv{A.xy + (cw + (long long)bitrev((uint32_t)j, A.n) * A.B) * Q, A.B, n, scr, ns, N};
+    QInfo qi{&A, cw, store, 0, j, G - 1};
     for (int k = 0; k < (1 << D); ++k) {
         const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
         const int e0 = A.ef[k];  // first all-frozen depth on this chain (D + 1: none)
@@ -271,7 +331,7 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
                 const QV<Q> x0 = lv.template get<Q>(a, p), x1 = lv.template get<Q>(a, p + S);
                 v[p] = gop ? q_plus<Q>(x0, x1, q_sym(Y, ns, ystart + p)) : q_minus<Q>(x0, x1);
             }
-            QSub<Q, S>::run(v, y, k * S, qi);
+            QSub<Q, S, G>::run(v, y, k * S, qi, lane);
         } else {
 #pragma unroll
             for (int j = 0; j < S; ++j) y[j] = 0;  // rate-0: symbols 0, re-encoding 0
@@ -313,8 +373,12 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
             }
         }
     }
-    if (A.xhat && store)
-        for (int i = 0; i < N; ++i) A.xhat[(long long)i * A.B + cw] = (uint8_t)q_sym(Y, ns, (int)bitrev((uint32_t)i, n));
+    // x_hat[i] is the root's half-split position bitrev(i): lane j holds the rows
+    // bitrev_n(j) + bitrev_{n-g}(t), t = its local position
+    if (A.xhat && store) {
+        uint8_t* xo = A.xhat + cw + (long long)bitrev((uint32_t)j, A.n) * A.B;
+        for (int t = 0; t < N; ++t) xo[(long long)bitrev((uint32_t)t, n) * A.B] = (uint8_t)q_sym(Y, ns, t);
+    }
 }
 
 }  // namespace pcub

@@ -125,6 +125,15 @@ def set_max_blocks_per_cu(b):
     _lib.check(_lib.lib().pcub_sc_set_max_blocks_per_cu(int(b)), "pcub_sc_set_max_blocks_per_cu")
 
 
+def set_qary_lanes(g):
+    """Lanes per codeword of the q-ary decode kernel (1, 2 or 4; reduced for short
+    codes).  Returns the previous setting."""
+    old = int(_lib.lib().pcub_sc_set_qary_lanes(int(g)))
+    if old < 0:
+        raise ValueError("q-ary lanes per codeword must be 1, 2 or 4")
+    return old
+
+
 def variants():
     """[(S, G, W)] per decode kernel variant: register-subtree values per lane,
     lanes per codeword, minimum waves per SIMD."""

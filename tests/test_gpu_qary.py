@@ -7,8 +7,18 @@ from tests.conftest import load_golden
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
+LANES = [1, 2, 4]  # lanes per codeword of the q-ary kernel
 
-def test_qsc_q4_n256_matches_reference():
+
+@pytest.fixture(params=LANES)
+def lanes(request):
+    from polarcub_amd import sc
+    old = sc.set_qary_lanes(request.param)
+    yield request.param
+    sc.set_qary_lanes(old)
+
+
+def test_qsc_q4_n256_matches_reference(lanes):
     from polarcub_amd import sc
     g = load_golden("qsc_q4_n256")
     code = sc.QaryCode(4, 256, g["frozen"])
@@ -22,7 +32,7 @@ def test_qsc_q4_n256_matches_reference():
     assert torch.equal(enc, xhat)
 
 
-def test_qary_q3_matches_reference():
+def test_qary_q3_matches_reference(lanes):
     from polarcub_amd import sc
     g = load_golden("qary_q3_n32")
     code = sc.QaryCode(3, 32, g["frozen"])
@@ -40,13 +50,14 @@ def test_qary_encode_matches_reference():
     assert np.array_equal(x.cpu().numpy(), g["x"])
 
 
-@pytest.mark.parametrize("q", [2, 3, 4, 5, 8])
-def test_qary_random_vs_oracle(q):
+@pytest.mark.parametrize("q", [2, 3, 4, 5, 6, 7, 8])
+def test_qary_random_vs_oracle(q, lanes):
     from oracle import orc
     from polarcub_amd import sc
     rng = np.random.default_rng(q)
-    for N, B in [(4, 7), (64, 300), (512, 1000)]:
+    for N, B in [(4, 7), (16, 33), (64, 300), (512, 1000)]:
         frozen = (rng.random(N) < 0.4).astype(np.uint8)
+        frozen[N // 2: N // 2 + N // 8] = 1  # an aligned rate-0 block
         xy = rng.random((B, N, q))
         xy[rng.random((B, N)) < 0.05] = 0.0
         code = sc.QaryCode(q, N, frozen)

@@ -62,6 +62,9 @@ struct McArgs {
     int K;
     int channel;       // 0 = BI-AWGN (param = sigma^2), 1 = BSC (param = p)
     double param;
+    double sigma;      // BI-AWGN: sqrt(sigma^2)
+    double inv2s2;     //          1 / (2 sigma^2)
+    double dens;       //          0.5 / sqrt(2 pi sigma^2) (uniform prior x Gaussian density)
 };
 
 // K uniform information bits per codeword: word w of codeword g is Philox
@@ -82,38 +85,59 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_info(McArgs A, uint32_t* info) 
     }
 }
 
-// Channel outputs as joint pairs, native [N][B][2]: element i of codeword g uses
-// Philox counter (g, kStreamChannel, i).
-__device__ void mc_channel_elem(const McArgs& A, const uint32_t* x, double2* xy, long long e) {
-    const long long i = e / A.B, b = e - i * A.B;
-    const uint64_t g = (uint64_t)(A.offset + b);
-    const uint32_t xb = (x[(i >> 5) * A.B + b] >> (i & 31)) & 1u;
-    const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)i, (uint32_t)A.seed,
-                        (uint32_t)(A.seed >> 32));
+// Channel outputs as joint pairs, native [N][B][2].  Elements 2j and 2j+1 of
+// codeword g share Philox counter (g, kStreamChannel, j): words 0-1 and 2-3 are
+// two 53-bit uniforms, and for BI-AWGN one Box-Muller transform yields both
+// normals (cos and sin branches).  A thread owns one codeword and walks element
+// pairs, so both of its stores are coalesced over the codeword-minor layout and
+// no 64-bit index division is needed.  sigma, 1/(2 sigma^2) and the density
+// constant come precomputed from the host.
+__device__ __forceinline__ double2 awgn_pair(const McArgs& A, uint32_t xb, double z) {
+    const double y = (xb ? -1.0 : 1.0) + A.sigma * z;
     double2 o;
-    if (A.channel == 0) {
-        const double s2 = A.param;
-        const double z = sqrt(-2.0 * log(u01(r.v[0], r.v[1]))) * cos(6.283185307179586 * u01(r.v[2], r.v[3]));
-        const double y = (xb ? -1.0 : 1.0) + sqrt(s2) * z;
-        const double c = 0.5 / sqrt(6.283185307179586 * s2);
-        o.x = c * exp(-((y - 1.0) * (y - 1.0)) / (2.0 * s2));
-        o.y = c * exp(-((y + 1.0) * (y + 1.0)) / (2.0 * s2));
-    } else {
-        const double p = A.param;
-        const uint32_t yb = xb ^ (u01(r.v[0], r.v[1]) <= p ? 1u : 0u);
-        // makeBSC table probs[y][x] = [[.5(1-p), .5p], [.5p, .5(1-p)]]
-        const double hi = 0.5 * (1.0 - p), lo = 0.5 * p;
-        o.x = yb ? lo : hi;
-        o.y = yb ? hi : lo;
-    }
-    xy[e] = o;
+    o.x = A.dens * exp(-((y - 1.0) * (y - 1.0)) * A.inv2s2);
+    o.y = A.dens * exp(-((y + 1.0) * (y + 1.0)) * A.inv2s2);
+    return o;
 }
 
-// grid-stride: the dispatch packet's grid size is 32-bit (N * B reaches 2^32 at N = 4096, B = 2^20)
+__device__ __forceinline__ double2 bsc_pair(const McArgs& A, uint32_t xb, double u) {
+    // makeBSC table probs[y][x] = [[.5(1-p), .5p], [.5p, .5(1-p)]]
+    const uint32_t yb = xb ^ (u <= A.param ? 1u : 0u);
+    const double hi = 0.5 * (1.0 - A.param), lo = 0.5 * A.param;
+    double2 o;
+    o.x = yb ? lo : hi;
+    o.y = yb ? hi : lo;
+    return o;
+}
+
+// grid: x over codewords, y strides over element pairs (a 2-D grid keeps every
+// dimension far below the 32-bit dispatch limits at N = 2^24).
 __global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_t* x, double2* xy) {
-    const long long total = (1LL << A.n) * A.B;
-    for (long long e = (long long)blockIdx.x * kMcBlock + threadIdx.x; e < total; e += (long long)gridDim.x * kMcBlock)
-        mc_channel_elem(A, x, xy, e);
+    const long long b = (long long)blockIdx.x * kMcBlock + threadIdx.x;
+    if (b >= A.B) return;
+    const uint64_t g = (uint64_t)(A.offset + b);
+    const long long N = 1LL << A.n;
+    const long long pairs = (N + 1) / 2;
+    for (long long j = blockIdx.y; j < pairs; j += gridDim.y) {
+        const long long i0 = 2 * j;
+        const uint32_t xw = x[(i0 >> 5) * A.B + b] >> (i0 & 31);  // bits i0, i0 + 1 (same word: i0 even)
+        const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)j, (uint32_t)A.seed,
+                            (uint32_t)(A.seed >> 32));
+        const double u0 = u01(r.v[0], r.v[1]), u1 = u01(r.v[2], r.v[3]);
+        double2 o0, o1;
+        if (A.channel == 0) {
+            const double rad = sqrt(-2.0 * log(u0));
+            double sn, cs;
+            sincos(6.283185307179586 * u1, &sn, &cs);
+            o0 = awgn_pair(A, xw & 1u, rad * cs);
+            o1 = awgn_pair(A, (xw >> 1) & 1u, rad * sn);
+        } else {
+            o0 = bsc_pair(A, xw & 1u, u0);
+            o1 = bsc_pair(A, (xw >> 1) & 1u, u1);
+        }
+        xy[i0 * A.B + b] = o0;
+        if (i0 + 1 < N) xy[(i0 + 1) * A.B + b] = o1;
+    }
 }
 
 // counters[0] += B, [1] += frame errors, [2] += bit errors (information bits)
@@ -148,17 +172,13 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_count(const uint32_t* dec, cons
 }
 
 unsigned grid_of(long long work) { return (unsigned)((work + kMcBlock - 1) / kMcBlock); }
-unsigned stride_grid(long long work) {
-    const long long g = (work + kMcBlock - 1) / kMcBlock;
-    return (unsigned)(g < (1 << 20) ? g : (1 << 20));
-}
 
 }  // namespace
 
 extern "C" int pcub_mc_info(uint64_t seed, int64_t offset, int64_t B, int32_t K, uint32_t* info_words, void* stream) {
     if (B < 0 || offset < 0 || K < 0 || (K > 0 && B > 0 && !info_words)) return PCUB_EINVAL;
     if (B == 0 || K == 0) return 0;
-    McArgs A{seed, offset, B, 0, K, 0, 0.0};
+    McArgs A{seed, offset, B, 0, K, 0, 0.0, 0.0, 0.0, 0.0};
     hipLaunchKernelGGL(k_mc_info, dim3(grid_of(B)), dim3(kMcBlock), 0, (hipStream_t)stream, A, info_words);
     return (int)hipGetLastError();
 }
@@ -170,9 +190,21 @@ extern "C" int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t
     if (channel == 1 && !(param >= 0.0 && param <= 1.0)) return PCUB_EINVAL;
     if (B == 0) return 0;
     if (!x_words || !xy) return PCUB_EINVAL;
-    McArgs A{seed, offset, B, log2N, 0, channel, param};
-    hipLaunchKernelGGL(k_mc_channel, dim3(stride_grid(((long long)1 << log2N) * B)), dim3(kMcBlock), 0,
-                       (hipStream_t)stream, A, x_words, (double2*)xy);
+    McArgs A{seed, offset, B, log2N, 0, channel, param, 0.0, 0.0, 0.0};
+    if (channel == 0) {
+        A.sigma = sqrt(param);
+        A.inv2s2 = 1.0 / (2.0 * param);
+        A.dens = 0.5 / sqrt(6.283185307179586 * param);
+    }
+    // ~16 k workgroups in total, y capped by the number of element pairs
+    const long long gx = (B + kMcBlock - 1) / kMcBlock;
+    const long long pairs = (((long long)1 << log2N) + 1) / 2;
+    long long gy = (16384 + gx - 1) / gx;
+    if (gy > pairs) gy = pairs;
+    if (gy > 65535) gy = 65535;
+    if (gx > 0x7fffffffLL) return PCUB_EINVAL;
+    hipLaunchKernelGGL(k_mc_channel, dim3((unsigned)gx, (unsigned)gy), dim3(kMcBlock), 0, (hipStream_t)stream, A,
+                       x_words, (double2*)xy);
     return (int)hipGetLastError();
 }
 

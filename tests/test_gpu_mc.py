@@ -68,3 +68,51 @@ def test_bsc_fer_agrees_with_reference_run():
     p_ref = g["meta"]["frame_errors"] / g["meta"]["trials"]
     sigma = math.sqrt(p_dev * (1 - p_dev) / g["meta"]["trials"])
     assert abs(p_dev - p_ref) <= 4 * sigma + 1e-3, (p_dev, p_ref)
+
+
+def _x_bits(code, info):
+    """x [N, B] u8 of the device encoder for native information words."""
+    from polarcub_amd import sc
+    xw = sc.encode_native(code, info).cpu().numpy().view(np.uint32)  # [ceil(N/32), B]
+    bits = (xw[:, None, :] >> np.arange(32, dtype=np.uint32)[None, :, None]) & 1
+    return bits.reshape(-1, xw.shape[1])[:code.N].astype(np.uint8)
+
+
+def test_awgn_channel_law(code):
+    """BI-AWGN pairs: the joint rows are 0.5 N(y; +-1, s2), so y = s2/2 ln(p0/p1) and
+    (1 - 2x) y ~ N(1, s2) whatever x; both Box-Muller branches (even / odd elements)
+    follow it and are uncorrelated."""
+    from polarcub_amd import mc
+    c, s2 = code
+    info, xy = mc.philox_batch(c, 5, 0, 2048, mc.CHANNEL_AWGN, s2)
+    xy = xy.cpu().numpy()
+    x = _x_bits(c, info)
+    y = 0.5 * s2 * np.log(xy[..., 0] / xy[..., 1])
+    z = ((1.0 - 2.0 * x) * y - 1.0) / math.sqrt(s2)  # ~ N(0, 1)
+    n = z.size
+    assert abs(z.mean()) < 5 / math.sqrt(n)
+    assert abs(z.var() - 1.0) < 5 * math.sqrt(2.0 / n)
+    for half in (z[0::2], z[1::2]):
+        assert abs(half.mean()) < 5 / math.sqrt(half.size)
+        assert abs(half.var() - 1.0) < 5 * math.sqrt(2.0 / half.size)
+    assert abs(np.mean(z[0::2] * z[1::2])) < 5 / math.sqrt(z[0::2].size)
+    # the density constant: p0 + p1 integrates the joint law, p0 = 0.5 phi(y - 1)
+    dens = 0.5 / math.sqrt(2 * math.pi * s2) * np.exp(-(y - 1.0) ** 2 / (2 * s2))
+    np.testing.assert_allclose(xy[..., 0], dens, rtol=1e-9, atol=1e-300)
+
+
+def test_bsc_channel_law(code):
+    """BSC pairs are makeBSC's rows for y = x ^ flip, flips ~ Bernoulli(p) on both branches."""
+    from polarcub_amd import mc
+    c, _ = code
+    p = 0.11
+    info, xy = mc.philox_batch(c, 6, 0, 1024, mc.CHANNEL_BSC, p)
+    xy = xy.cpu().numpy()
+    x = _x_bits(c, info)
+    hi, lo = 0.5 * (1 - p), 0.5 * p
+    yb = (xy[..., 0] == lo).astype(np.uint8)
+    assert np.all(np.where(yb == 1, xy[..., 1] == hi, (xy[..., 0] == hi) & (xy[..., 1] == lo)))
+    flips = yb ^ x
+    for half in (flips[0::2], flips[1::2]):
+        f = half.mean()
+        assert abs(f - p) < 5 * math.sqrt(p * (1 - p) / half.size)

@@ -51,6 +51,7 @@ struct DelArgs {
     uint32_t* xhat;         // [ceil(N/32)][B] or null
     const uint32_t* fval_cw;  // [ceil(N/32)][B] per-codeword frozen values (export mode), or null
     double* leaf;           // [N][B] compact normalised leaves (export mode)
+    int rw;                 // > 0: words per codeword of the bit-packed received words in LDS
 };
 
 // XSub (sc_bin_body.h) for the export mode: no rate-0 node is skipped and the two
@@ -221,13 +222,38 @@ __global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
     const long long c = valid ? cw : A.B - 1;  // padding groups decode a duplicate, store nothing
     for (int i = threadIdx.x; i < CPB * WPC; i += kBlock) xs[i] = 0;
 
+    // Received words, bit-packed into LDS (rw > 0, the launcher's choice when the
+    // group's words fit): each wave packs whole codewords with coalesced byte loads
+    // and a ballot per 64 symbols, so the guard-band parse below probes 32 symbols
+    // per LDS read instead of walking zero runs one dependent global load at a time.
+    extern __shared__ uint32_t rxb[];
+    const bool pk = A.rw > 0;
+    if (pk) {
+        for (int gg = threadIdx.x >> 6; gg < CPB; gg += kBlock / 64) {
+            long long cg = (long long)blockIdx.x * CPB + gg;
+            cg = cg < A.B ? cg : A.B - 1;
+            const uint8_t* row = A.rx + cg * (long long)A.stride;
+            int ln = A.rx_len[cg];
+            ln = ln < 0 ? 0 : (ln > A.stride ? A.stride : ln);
+            for (int base = 0; base < A.rw * 32; base += 64) {
+                const int i = base + lane;
+                const unsigned long long msk = __ballot(i < ln && row[i] == 1);
+                const int wi = (base >> 5) + (lane & 1);
+                if (lane < 2 && wi < A.rw) rxb[gg * A.rw + wi] = (uint32_t)(msk >> (32 * lane));
+            }
+        }
+        __syncthreads();
+    }
+
     const uint8_t* w = A.rx + c * (long long)A.stride;
+    const uint32_t* pw = rxb + (pk ? g * A.rw : 0);
     int len = A.rx_len[c];
     len = len < 0 ? 0 : (len > A.stride ? A.stride : len);
-    auto bit = [w](int i) { return (int)w[i]; };
+    auto bit = [w, pw, pk](int i) { return pk ? (int)((pw[i >> 5] >> (i & 31)) & 1u) : (int)w[i]; };
     const int t = (int)bitrev((uint32_t)p, TB);
     int s, m;
-    segment_of(bit, len, TB, t, s, m);
+    if (pk) segment_of_packed(pw, len, TB, t, s, m);
+    else segment_of(bit, len, TB, t, s, m);
 
     DelCtx<T, EXP> cx;
     cx.A = A;
@@ -322,7 +348,12 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     A.leaf = leaf;
     const long long cpb = kBlock >> (n - n0);
     const long long grid = (B + cpb - 1) / cpb;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, A);
+    // bit-packed received words in LDS when the group's words fit in 32 KiB (always for
+    // the 64-trellis shapes; very long padded rows of small codes parse from HBM)
+    const long long rw = ((long long)stride + 31) / 32;
+    A.rw = (cpb * rw * 4 <= 32768) ? (int)rw : 0;
+    const size_t lds = A.rw ? (size_t)(cpb * rw * 4) : 0;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
 

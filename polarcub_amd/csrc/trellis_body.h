@@ -240,4 +240,53 @@ PCUB_HD void segment_of(const BitF& bit, int len, int levels, int t, int& s, int
     m = e - a;
 }
 
+// The same parse on a bit-packed received word (bit i of word i >> 5 = symbol i == 1,
+// bits past the word's length 0): each probe covers 32 symbols, so a guard band of
+// zeros is crossed in a few LDS reads instead of one dependent byte load per symbol.
+// first symbol 1 in [a, e), or e
+PCUB_HD int first_one(const uint32_t* w, int a, int e) {
+    while (a < e) {
+        const uint32_t x = w[a >> 5] >> (a & 31);
+        if (x) {
+            const int i = a + __builtin_ctz(x);
+            return i < e ? i : e;
+        }
+        a = (a | 31) + 1;
+    }
+    return e;
+}
+
+// last symbol 1 in [a, e); one must exist
+PCUB_HD int last_one(const uint32_t* w, int e) {
+    int b = e - 1;
+    for (;;) {
+        const uint32_t x = w[b >> 5] << (31 - (b & 31));
+        if (x) return b - __builtin_clz(x);
+        b = (b & ~31) - 1;
+    }
+}
+
+PCUB_HD void trim_range_packed(const uint32_t* w, int& s, int& e) {
+    const int a = first_one(w, s, e);
+    if (a == e) {
+        s = e = a;
+        return;
+    }
+    e = last_one(w, e) + 1;
+    s = a;
+}
+
+PCUB_HD void segment_of_packed(const uint32_t* w, int len, int levels, int t, int& s, int& m) {
+    int a = 0, e = len;
+    trim_range_packed(w, a, e);
+    for (int k = levels - 1; k >= 0; --k) {
+        const int h = (e - a) / 2;
+        if ((t >> k) & 1) a += h;
+        else e = a + h;
+        trim_range_packed(w, a, e);
+    }
+    s = a;
+    m = e - a;
+}
+
 }  // namespace pcub

@@ -223,3 +223,39 @@ extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, lon
 }
 
 extern "C" void emu_set_n02(int on) { use_n02 = on != 0; }
+
+// segment_of on bytes vs segment_of_packed on the packed word (the kernel's parse), for
+// random words with long zero runs (guard bands) and every trellis of 1..6 levels.
+// Returns the number of disagreeing (word, levels, t) cases.
+extern "C" long long emu_check_segments(uint64_t seed, int words) {
+    uint64_t st = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto rnd = [&st]() {
+        st ^= st << 13;
+        st ^= st >> 7;
+        st ^= st << 17;
+        return st;
+    };
+    long long bad = 0;
+    for (int it = 0; it < words; ++it) {
+        const int len = (int)(rnd() % 700);
+        std::vector<uint8_t> w(len + 1, 0);
+        int i = 0;
+        while (i < len) {
+            const int run = (int)(rnd() % (rnd() % 4 == 0 ? 90 : 4)) + 1;
+            const uint8_t v = (uint8_t)(rnd() % 3 == 0 ? 0 : (rnd() & 1));
+            for (int j = 0; j < run && i < len; ++j, ++i) w[i] = (rnd() % 5 == 0) ? (uint8_t)(rnd() & 1) : v;
+        }
+        std::vector<uint32_t> pk((len + 31) / 32 + 1, 0);
+        for (int j = 0; j < len; ++j)
+            if (w[j] == 1) pk[j >> 5] |= 1u << (j & 31);
+        auto bit = [&w](int j) { return (int)w[j]; };
+        for (int lv = 1; lv <= 6; ++lv)
+            for (int t = 0; t < (1 << lv); ++t) {
+                int s0, m0, s1, m1;
+                pcub::segment_of(bit, len, lv, t, s0, m0);
+                pcub::segment_of_packed(pk.data(), len, lv, t, s1, m1);
+                bad += (s0 != s1 || m0 != m1) ? 1 : 0;
+            }
+    }
+    return bad;
+}

@@ -96,3 +96,12 @@ def test_n02_random_vs_oracle(n):
             assert list(info[i]) == ir and list(xhat[i]) == xr, i
     finally:
         emu().emu_set_n02(0)
+
+
+def test_packed_segment_parse_matches_byte_parse():
+    """The kernel parses guard bands on the bit-packed received word (segment_of_packed):
+    same (start, length) as the byte-wise removeDeletionGuardBands restatement for every
+    trellis of 1..6 levels on random words with long zero runs."""
+    L = emu()
+    L.emu_check_segments.restype = ctypes.c_longlong
+    assert L.emu_check_segments(ctypes.c_uint64(12345), 3000) == 0

@@ -95,6 +95,11 @@ struct DelCtx {
     uint32_t acc;
     int nacc;
     int infow;
+    // T == 64, decode mode: the group's memoryless subtrees are decoded by wave 0 with
+    // 16 lanes per codeword (see subtree()); exchange buffers in LDS
+    double* xv;               // [4][64] collapsed values, one row per wave (= codeword)
+    unsigned long long* xb;   // [4] ballots of the encoding bits, one per local index
+    unsigned long long* xub;  // [4] decisions per codeword
 
     // bits [k*T, (k+1)*T) of a bit vector whose word i is w[i * stride]
     PCUB_HD uint64_t window(const uint32_t* w, long long stride = 1) const {
@@ -119,6 +124,38 @@ struct DelCtx {
         } else if (fm == WM) {  // rate-0 node: decisions are the frozen values
             ub = fv;
             y = frozen_local<1, T>(fv, lane & (T - 1));
+        } else if constexpr (T == 64) {
+            // One codeword per wave is the trellis stages' layout, but a length-64
+            // subtree decoded across one wave's lanes (XSub<64>) spends a full wave op
+            // on every node.  So the four codewords' collapsed rows go through LDS to
+            // one wave, which decodes all four at once with 16 lanes per codeword (lane
+            // j of group c owns positions j + 16t, SubV<4, 0, 16>: the binary
+            // kernel's schedule), and hands back the encoding bits and decisions.
+            // fm / fv are the same for the whole group (per-codeword frozen values
+            // exist only in export mode), so every wave takes this branch together.
+            const int wv = threadIdx.x >> 6;
+            xv[wv * 64 + lane] = v;
+            __syncthreads();
+            // (measured: wave 0 with four codewords beats two waves with two each, and
+            // beats rotating the decoding wave over the group's waves)
+            if (wv == 0) {
+                const int c = lane >> 4, j = lane & 15;
+                double vv[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) vv[t] = xv[c * 64 + j + 16 * t];
+                uint64_t ubl = 0;
+                const uint32_t bits = SubV<4, 0, 16>::run(vv, ubl, fm, fv, lane);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const unsigned long long bal = __ballot((bits >> t) & 1u);
+                    if (lane == 0) xb[t] = bal;
+                }
+                if (j == 0) xub[c] = ubl;
+            }
+            __syncthreads();
+            // position p = lane is local index p >> 4 of lane (wv * 16 + (p & 15))
+            y = (uint32_t)(xb[lane >> 4] >> (wv * 16 + (lane & 15))) & 1u;
+            ub = xub[wv];
         } else {
             y = XSub<T, 0>::run(v, ub, fm, fv, lane) & 1u;
         }
@@ -255,7 +292,12 @@ __global__ __launch_bounds__(kBlock) void k_sc_del(DelArgs A) {
     if (pk) segment_of_packed(pw, len, TB, t, s, m);
     else segment_of(bit, len, TB, t, s, m);
 
+    __shared__ double xv[(T == 64 && !EXP) ? 256 : 1];
+    __shared__ unsigned long long xb[4], xub[4];
     DelCtx<T, EXP> cx;
+    cx.xv = xv;
+    cx.xb = xb;
+    cx.xub = xub;
     cx.A = A;
     cx.cw = cw;
     cx.leader = valid && p == 0;

@@ -15,13 +15,21 @@ timed region.  One step = one decode launch over the whole per-GPU batch.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload awgn|deletion|qary] [--batch B]
 
-Multi-GPU: launched by torch.distributed.run, one rank per GPU; rank r decodes its
-own batch (global codewords [r*B, (r+1)*B), no data-path collective); one RCCL
-all_reduce of the error counters and a max-reduce of the elapsed time at the end.
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) this
+process is one rank; started directly with --gpus N > 1 it launches the N ranks itself
+(torch.distributed.run as a child process, before anything touches the GPU) and exits
+with their status.  Rank r decodes global codewords [r*B, (r+1)*B) (no data-path
+collective); one RCCL all_reduce of the error counters, a max-reduce of the elapsed
+time and an all_gather of the per-rank times at the end.
+
+--workload stub is the same rank logic on the CPU (gloo, oracle decode of N=64 BSC
+codewords keyed by global codeword index): the multi-rank test of the launcher.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,11 +50,24 @@ def log(*a):
 
 
 def host_cores():
+    """(threads to use, description): every core in this process's affinity mask, capped by
+    the cgroup CPU quota when one is set (more threads than the quota only time-slice)."""
     try:
-        c = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        c = os.cpu_count() or 1
-    return max(1, min(c, 16))
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    used = aff if quota is None else min(aff, quota)
+    desc = "%d host threads (sched_getaffinity %d cores, cgroup cpu quota %s)" % (
+        used, aff, "none" if quota is None else "%d CPUs" % quota)
+    return max(1, used), desc
 
 
 def measured_traffic(tag, batch):
@@ -81,7 +102,8 @@ class Awgn:
         sc.set_max_blocks_per_cu(a.max_blocks)
         self.dec = sc.BinaryDecoder(self.code)
         # global codewords [rank*B, (rank+1)*B), Philox keyed by (seed, codeword index)
-        self.info_w, self.xy = mc.philox_batch(self.code, a.seed, rank * self.B, self.B, mc.CHANNEL_AWGN, self.sigma2)
+        self.offset = mc.rank_offset(rank, self.B)
+        self.info_w, self.xy = mc.philox_batch(self.code, a.seed, self.offset, self.B, mc.CHANNEL_AWGN, self.sigma2)
         self.rank = rank
         self.outs = (torch.empty((self.code.info_words, self.B), dtype=torch.int32, device=device),
                      None if a.no_xhat else torch.empty((self.code.n_words, self.B), dtype=torch.int32, device=device),
@@ -100,10 +122,10 @@ class Awgn:
         encoder -> BI-AWGN -> decode -> counters) over this rank's codewords, in chunks of up to
         2^20 codewords: seconds of the second (warm: workspace cached) run."""
         chunk = min(self.B, 1 << 20)
-        mc.run_bin(self.code, self.a.seed, self.rank * self.B, self.B, mc.CHANNEL_AWGN, self.sigma2, chunk=chunk)
+        mc.run_bin(self.code, self.a.seed, self.offset, self.B, mc.CHANNEL_AWGN, self.sigma2, chunk=chunk)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        mc.run_bin(self.code, self.a.seed, self.rank * self.B, self.B, mc.CHANNEL_AWGN, self.sigma2, chunk=chunk)
+        mc.run_bin(self.code, self.a.seed, self.offset, self.B, mc.CHANNEL_AWGN, self.sigma2, chunk=chunk)
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
@@ -138,7 +160,7 @@ class Awgn:
         t0 = time.perf_counter()
         orc.decode_bin(sample[:64], code.frozen_mask, code.frozen_values)
         per_cw = (time.perf_counter() - t0) / 64
-        cores = host_cores()
+        cores, cdesc = host_cores()
         reps = max(1, int(round(seconds / (per_cw * ncw))))
 
         def work(i):
@@ -153,7 +175,7 @@ class Awgn:
         dt = time.perf_counter() - t0
         return {"value": total / dt, "unit": "codewords/s", "cores": cores, "kind": "port",
                 "sample": "%d codewords x %d passes of the bench's own synthetic N=%d inputs, oracle/sc_oracle.c "
-                          "on %d threads (%.1f CPU-s)" % (ncw, reps, code.N, cores, dt * cores)}
+                          "on %s (%.1f CPU-s)" % (ncw, reps, code.N, cdesc, dt * cores)}
 
 
 class Deletion:
@@ -207,20 +229,39 @@ class Deletion:
                     "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
 
     def cpu_baseline(self, seconds=10.0):
-        """oracle/trellis_oracle.py (pure Python restatement, one thread) on a bounded sample."""
-        from oracle import trellis_oracle as tro
-        rx = self.rx[:4096].cpu().numpy()
-        ln = self.rx_len[:4096].cpu().numpy()
+        """oracle/trellis_oracle.py (pure Python restatement) in one process per host core
+        (the GIL rules out threads), each on its own slice of a bounded sample."""
+        from concurrent.futures import ProcessPoolExecutor
+        import multiprocessing as mp
+        cores, cdesc = host_cores()
+        ncw = min(self.B, 256 * cores)
+        rx = self.rx[:ncw].cpu().numpy()
+        ln = self.rx_len[:ncw].cpu().numpy()
+        words = [list(map(int, rx[i, :ln[i]])) for i in range(ncw)]
         fm, fv = self.code.frozen_mask, self.code.frozen_values
-        t0 = time.perf_counter()
-        done = 0
-        while time.perf_counter() - t0 < seconds and done < rx.shape[0]:
-            tro.decode_deletion(list(map(int, rx[done, :ln[done]])), self.n, self.n0, self.pd, fm, fv)
-            done += 1
-        dt = time.perf_counter() - t0
-        return {"value": done / dt, "unit": "codewords/s", "cores": 1, "kind": "port",
-                "sample": "first %d codewords of the bench's own received words, oracle/trellis_oracle.py "
-                          "(pure Python, 1 thread, %.1f s)" % (done, dt)}
+        parts = [words[(i * ncw) // cores:((i + 1) * ncw) // cores] for i in range(cores)]
+        with ProcessPoolExecutor(cores, mp_context=mp.get_context("spawn")) as ex:
+            list(ex.map(_del_oracle_part, [(p[:1], self.n, self.n0, self.pd, fm, fv, 0.0) for p in parts]))  # warm
+            t0 = time.perf_counter()
+            done = sum(ex.map(_del_oracle_part, [(p, self.n, self.n0, self.pd, fm, fv, seconds) for p in parts]))
+            dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "codewords/s", "cores": cores, "kind": "port",
+                "sample": "%d of the bench's own received words (time-bounded, %.0f s), oracle/trellis_oracle.py "
+                          "(pure Python) in one process per thread on %s" % (done, seconds, cdesc)}
+
+
+def _del_oracle_part(args):
+    words, n, n0, pd, fm, fv, seconds = args
+    sys.path.insert(0, ROOT)
+    from oracle import trellis_oracle as tro
+    t0 = time.perf_counter()
+    done = 0
+    for w in words:
+        tro.decode_deletion(w, n, n0, pd, fm, fv)
+        done += 1
+        if seconds and time.perf_counter() - t0 > seconds:
+            break
+    return done
 
 
 class Qary:
@@ -272,24 +313,105 @@ class Qary:
                     "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
 
     def cpu_baseline(self, seconds=10.0):
+        """oracle/sc_oracle.c q-ary recursion on the host threads (ctypes releases the GIL)."""
+        from concurrent.futures import ThreadPoolExecutor
+
         from oracle import orc
         orc.lib()
-        ncw = 2048
+        cores, cdesc = host_cores()
+        ncw = 4096
         sample = self.xy[:, :ncw, :].permute(1, 0, 2).contiguous().cpu().numpy()
         t0 = time.perf_counter()
-        reps = 0
-        while time.perf_counter() - t0 < seconds:
-            orc.decode_qary(self.q, sample, self.code.frozen_mask)
-            reps += 1
+        orc.decode_qary(self.q, sample[:64], self.code.frozen_mask)
+        per_cw = (time.perf_counter() - t0) / 64
+        reps = max(1, int(round(seconds * cores / (per_cw * ncw))))
+
+        def work(i):
+            part = sample[(i * ncw) // cores:((i + 1) * ncw) // cores]
+            for _ in range(reps):
+                orc.decode_qary(self.q, part, self.code.frozen_mask)
+            return part.shape[0] * reps
+
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(cores) as ex:
+            total = sum(ex.map(work, range(cores)))
         dt = time.perf_counter() - t0
-        return {"value": ncw * reps / dt, "unit": "codewords/s", "cores": 1, "kind": "port",
-                "sample": "%d codewords x %d passes, oracle/sc_oracle.c q-ary, 1 thread" % (ncw, reps)}
+        return {"value": total / dt, "unit": "codewords/s", "cores": cores, "kind": "port",
+                "sample": "%d codewords x %d passes of the bench's own inputs, oracle/sc_oracle.c q-ary on %s"
+                          % (ncw, reps, cdesc)}
 
 
-WORKLOADS = {"awgn": Awgn, "deletion": Deletion, "qary": Qary}
+class Stub:
+    """The multi-rank logic of this script on the CPU (gloo): N=64 binary SC over BSC(0.11)
+    decoded by the CPU oracle; codeword g's information bits and channel flips are drawn
+    from a generator keyed by (seed, g), and rank r owns global codewords
+    [rank_offset(r, B), rank_offset(r, B) + B) exactly as the GPU workloads do.  Used by
+    tests/test_bench_launch.py; never a bench line."""
+    kernel = "oracle"
+
+    def __init__(self, a, device, rank):
+        from oracle import orc
+        self.a, self.orc = a, orc
+        self.n, self.N, self.B = 6, 64, a.batch
+        self.K = self.N // 2
+        self.frozen = construction.bhattacharyya_frozen(self.n, self.K, 0.5)
+        self.fval = np.zeros(self.N, np.uint8)
+        off = mc.rank_offset(rank, self.B)
+        p = 0.11
+        table = np.array([[0.5 * (1 - p), 0.5 * p], [0.5 * p, 0.5 * (1 - p)]])
+        self.info = np.zeros((self.B, self.K), np.uint8)
+        self.xy = np.zeros((self.B, self.N, 2))
+        for b in range(self.B):
+            g = np.random.default_rng([a.seed, off + b])
+            self.info[b] = g.integers(0, 2, self.K)
+            x = orc.encode_bin(self.info[b], self.frozen, fval=self.fval)
+            y = x ^ (g.random(self.N) < p).astype(np.uint8)
+            self.xy[b] = table[y]
+        self.out = None
+
+    def step(self):
+        self.out = self.orc.decode_bin(self.xy, self.frozen, self.fval)[0]
+
+    def errors(self):
+        d = self.out != self.info
+        return int(d.any(axis=1).sum()), int(d.sum())
+
+    def bytes_alg(self):
+        return 16 * self.N + self.N // 8 + self.K // 8
+
+    def tag(self):
+        return "stub"
+
+    def describe(self, world):
+        return dict(metric="stub: decoded codewords/sec of the CPU oracle (launcher test, not a bench line)",
+                    dtype="f64", data="synthetic BSC(0.11), generator keyed by global codeword index",
+                    config={"workload": "stub N=64 K=32 BSC(0.11) on the CPU oracle", "N": self.N, "K": self.K,
+                            "batch_per_gpu": self.B, "parallelism": "dp%d over gloo" % world})
 
 
-def main():
+WORKLOADS = {"awgn": Awgn, "deletion": Deletion, "qary": Qary, "stub": Stub}
+
+
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(a, argv):
+    """--gpus N > 1 outside torch.distributed.run: start the N ranks as one child
+    torch.distributed.run process (this process has not touched the GPU and never does),
+    pass its output through, return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(a.master_port or _free_port()),
+           os.path.abspath(__file__)] + argv
+    log("bench: launching %d ranks: %s" % (a.gpus, " ".join(cmd)))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -308,54 +430,81 @@ def main():
     ap.add_argument("--variant", type=int, default=None, help="binary decode kernel variant (default: the library's)")
     ap.add_argument("--max-blocks", type=int, default=0, help="cap decode workgroups per CU (0 = occupancy)")
     ap.add_argument("--seed", type=int, default=20250204)
+    ap.add_argument("--master-port", type=int, default=0, help="rendezvous port when launching ranks (0 = free port)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-xhat", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end Monte-Carlo leg (profiling: only the timed decode launches)")
-    a = ap.parse_args()
+    return ap
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    ap = build_parser()
+    a = ap.parse_args(argv)
 
     world, rank, local = mc.dist_env()
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(device)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(a, argv)
+    if world != a.gpus and world > 1:
+        log("bench: WORLD_SIZE=%d differs from --gpus %d; reporting the launched world" % (world, a.gpus))
+    on_gpu = a.workload != "stub"
+    if on_gpu:
+        device = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(device)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=device)
+        sync = torch.cuda.synchronize
+    else:
+        device = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+
+        def sync():
+            pass
+    coll_dev = device if (on_gpu and world > 1) else None
 
     t0 = time.time()
     w = WORKLOADS[a.workload](a, device, rank)
-    torch.cuda.synchronize()
+    sync()
     log("rank %d: %s inputs for %d codewords generated in %.1f s" % (rank, a.workload, w.B, time.time() - t0))
 
     for _ in range(a.warmup):
         w.step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
 
-    stream = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    evs = None
+    if on_gpu:
+        stream = torch.cuda.current_stream()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     t_start = time.perf_counter()
     for i in range(a.steps):
-        evs[i][0].record(stream)
+        if evs:
+            evs[i][0].record(stream)
         w.step()
-        evs[i][1].record(stream)
-    torch.cuda.synchronize()
+        if evs:
+            evs[i][1].record(stream)
+    sync()
+    t_local = time.perf_counter() - t_start  # this rank's own decode time
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t_start
-    kern_ms = [x.elapsed_time(y) for x, y in evs]
+    kern_ms = [x.elapsed_time(y) for x, y in evs] if evs else [t_local * 1e3 / max(1, a.steps)]
 
     fe, be = w.errors()  # of the last decode (identical every step)
-    counters, elapsed = mc.reduce_counters([w.B, fe, be, 0], elapsed, device if world > 1 else None)
+    counters, elapsed = mc.reduce_counters([w.B, fe, be, 0], elapsed, coll_dev)
+    per_rank = mc.gather_floats([t_local, float(np.mean(kern_ms)), w.B], coll_dev)
     total_cw = counters[0] * a.steps
     value = total_cw / elapsed
     e2e = None
     if hasattr(w, "end_to_end") and not a.no_e2e:
         if world > 1:
             dist.barrier()
-        _, e2e_s = mc.reduce_counters([0], w.end_to_end(), device if world > 1 else None)
+        _, e2e_s = mc.reduce_counters([0], w.end_to_end(), coll_dev)
         e2e = counters[0] / e2e_s
 
     if rank == 0:
@@ -380,20 +529,26 @@ def main():
             "config": d["config"],
             "fer": counters[1] / counters[0],
             "frame_errors": counters[1],
+            "bit_errors": counters[2],
+            "codewords_per_step": counters[0],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": w.kernel, "kernel_ms": float(np.mean(kern_ms)), "bytes_alg_per_cw": b_alg},
+            "per_rank": [{"rank": r, "codewords": int(v[2]), "value": v[2] * a.steps / v[0],
+                          "kernel_ms": v[1], "hbm_frac": b_alg * v[2] / (v[1] / 1e3) / 1e9 / HBM_PEAK_GBS}
+                         for r, v in enumerate(per_rank)],
         }
         if e2e is not None:
             rec["mc_end_to_end"] = {"value": e2e, "unit": "codewords/s",
                                     "what": "pcub_mc_run_bin: info bits + encode + channel + decode + counters, "
                                             "all on device, same codewords"}
-        if world == 1 and not a.no_cpu:
+        if world == 1 and not a.no_cpu and hasattr(w, "cpu_baseline"):
             rec["cpu_baseline"] = w.cpu_baseline()
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

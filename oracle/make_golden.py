@@ -418,6 +418,46 @@ def fx_harness(R, timing):
     save("harness_bsc_n64", dict(N=N, trials=T, global_seed=seed, p=0.11, line=line), frozen=g["frozen"])
 
 
+def fx_harness_verbose(R, timing):
+    """encodeDecodeSimulation with verbosity=1 (BinaryPolarEncoderDecoder.py:374-385): the
+    per-error printout (information as a Python list, decoded/encoded as numpy arrays)."""
+    import contextlib
+    import io
+    BMD, BPED = R["BMD"], R["BPED"]
+    g = np.load(os.path.join(OUT, "bsc_n64.npz"))
+    frozen = set(int(i) for i in np.nonzero(g["frozen"])[0])
+    N, T, seed = 64, 40, 9
+    xy_dist = BMD.makeBSC(0.11)
+
+    def make_x():
+        xd = BMD.BinaryMemorylessDistribution()
+        xd.probs.append([xy_dist.calcXMarginal(0), xy_dist.calcXMarginal(1)])
+        return xd.makeBinaryMemorylessVectorDistribution(N, None)
+
+    def channel(codeword):
+        out = []
+        for x in codeword:
+            rnd = random.random()
+            s = 0.0
+            for y in range(len(xy_dist.probs)):
+                if s + xy_dist.probXGivenY(x, y) >= rnd:
+                    out.append(y)
+                    break
+                s += xy_dist.probXGivenY(x, y)
+        return out
+
+    def make_xy(received):
+        return xy_dist.makeBinaryMemorylessVectorDistribution(len(received), received)
+
+    random.seed(seed)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        BPED.encodeDecodeSimulation(N, make_x, lambda e: e, channel, make_xy, T, frozen, verbosity=1)
+    out = buf.getvalue()
+    print("  reference verbose run: %d lines" % len(out.splitlines()))
+    save("harness_verbose", dict(N=N, trials=T, global_seed=seed, p=0.11, stdout=out), frozen=g["frozen"])
+
+
 def deletion_closures(R, n, n0, pd, xi, ones, channel_seed):
     """The main_deletion.py:17-59 closures, rebuilt from the reference modules (main_deletion.py
     itself runs main() on import)."""
@@ -780,6 +820,169 @@ def fx_construct_bin(R, timing):
          **arrays)
 
 
+def _qsc_channel_closure(qsc):
+    """test3.py:35-55 channel: one global random.random() per symbol, cumulative P(y|x)."""
+    def channel(codeword):
+        out = []
+        for x in codeword:
+            rnd = random.random()
+            s = 0.0
+            for y in range(len(qsc.probs)):
+                if s + qsc.probXGivenY(int(x), y) >= rnd:
+                    out.append(y)
+                    break
+                s += qsc.probXGivenY(int(x), y)
+        return out
+    return channel
+
+
+def _qary_tv_pe(R, n, L, xy_dist, x_dist=None):
+    """calcTVAndPe_degradingUpgrading (ScalarDistributions/QaryMemorylessDistribution.py:934-991)
+    through its own .npy cache in a temporary directory (it returns None without one)."""
+    import tempfile
+    QMD = R["QMD"]
+    with tempfile.TemporaryDirectory() as d:
+        tv, pe = QMD.calcTVAndPe_degradingUpgrading(n, L, x_dist, xy_dist, d + "/")
+    return np.asarray(tv, np.float64), np.asarray(pe, np.float64)
+
+
+def fx_construct_qary(R, timing):
+    """q-ary degrading construction (section 8(f) rank 3): the reference's own
+    QaryMemorylessDistribution.degrade (dynamic: one-hot binary channels degraded to
+    M = floor(L^(1/(q-1))) letters, product re-indexing) on polar-transformed QSC/QEC
+    channels, whole-tree Pe vectors (calcTVAndPe_degradingUpgrading) and the frozen sets of
+    frozenSetFromTVAndPe, including the C4 code: q=4, n=8, L=64, QSC(0.11),
+    numInfoIndices=127 (K=128, QaryPolarEncoderDecoder.py:1173-1176 off-by-one)."""
+    QMD, QPED = R["QMD"], R["QPED"]
+    arrays, cases, trees = {}, [], []
+    chans = {"qsc3": QMD.makeQSC(3, 0.2), "qsc4": QMD.makeQSC(4, 0.11), "qec3": QMD.makeQEC(3, 0.3),
+             "qsc5": QMD.makeQSC(5, 0.15)}
+    for cname, ch in chans.items():
+        variants = {"": ch, "m": ch.minusTransform(), "p": ch.plusTransform()}
+        if ch.q <= 3:
+            variants["mp"] = variants["m"].plusTransform()
+        for vname, d0 in variants.items():
+            case = cname + ("_" + vname if vname else "")
+            arrays[case + "_in"] = np.array(d0.probs, np.float64)
+            for L in (4, 9, 16, 64):
+                import copy
+                o = copy.deepcopy(d0).degrade(L)
+                arrays["%s_deg%d" % (case, L)] = np.array(o.probs, np.float64).reshape(-1, ch.q)
+            cases.append(case)
+    for tname, q, n, L, p, kinfo in (("qsc3_n4_L16", 3, 4, 16, 0.2, None), ("qsc4_n3_L27", 4, 3, 27, 0.11, None),
+                                     ("qsc4_n5_L64", 4, 5, 64, 0.11, 15), ("qsc2_n6_L16", 2, 6, 16, 0.11, None),
+                                     ("qsc4_n8_L64", 4, 8, 64, 0.11, 127)):
+        t0 = time.time()
+        ch = QMD.makeQSC(q, p)
+        tv, pe = _qary_tv_pe(R, n, L, ch)
+        timing["construct_qary_%s_s" % tname] = time.time() - t0
+        bound = 0.1
+        fz = QPED.frozenSetFromTVAndPe(tv, pe, None if kinfo is not None else bound, kinfo)
+        mask = np.zeros(1 << n, np.uint8)
+        mask[sorted(fz)] = 1
+        arrays[tname + "_tv"] = tv
+        arrays[tname + "_pe"] = pe
+        arrays[tname + "_frozen"] = mask
+        trees.append({"name": tname, "q": q, "n": n, "L": L, "p": p, "numInfoIndices": kinfo,
+                      "bound": None if kinfo is not None else bound, "K": int((1 << n) - mask.sum()),
+                      "seconds": round(time.time() - t0, 1)})
+        print("  tree %s: K=%d (%.1f s)" % (tname, (1 << n) - mask.sum(), time.time() - t0))
+    save("construct_qary", {"cases": cases, "trees": trees,
+                            "note": "reference QaryMemorylessDistribution.degrade / calcTVAndPe_degradingUpgrading / "
+                                    "QaryPolarEncoderDecoder.frozenSetFromTVAndPe; xDistribution=None (TV=0)"},
+         **arrays)
+
+
+def fx_qary_harness(R, timing):
+    """The reference's q-ary Monte-Carlo driver (QaryPolarEncoderDecoder.encodeDecodeSimulation,
+    QaryPolarEncoderDecoder.py:935-982) with the test3.py:21-70 closures and a seeded global
+    channel RNG; records the printed line and the per-trial words to replay it."""
+    import contextlib
+    import io
+    QMD, QPED = R["QMD"], R["QPED"]
+    g = np.load(os.path.join(OUT, "construct_qary.npz"))
+    out, runs = {}, []
+    for name, q, n, p, T, seed, fkey in (("q4_n5", 4, 5, 0.11, 300, 11, "qsc4_n5_L64_frozen"),
+                                         ("q3_n4", 3, 4, 0.2, 400, 12, "qsc3_n4_L16_frozen")):
+        N = 1 << n
+        frozen = set(int(i) for i in np.nonzero(g[fkey])[0])
+        qsc = QMD.makeQSC(q, p)
+
+        def make_x(q=q, qsc=qsc, N=N):
+            xd = QMD.QaryMemorylessDistribution(q)
+            xd.probs = [qsc.calcXMarginals()]
+            return xd.makeQaryMemorylessVectorDistribution(N, None)
+
+        def make_xy(rx, qsc=qsc):
+            return qsc.makeQaryMemorylessVectorDistribution(len(rx), rx)
+
+        random.seed(seed)
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            QPED.encodeDecodeSimulation(q, N, make_x, lambda e: e, _qsc_channel_closure(qsc), make_xy, T, frozen)
+        line = buf.getvalue().strip().splitlines()[-1]
+        print("  reference q-ary printed:", line)
+        runs.append(dict(name=name, q=q, n=n, p=p, trials=T, global_seed=seed, frozen_key=fkey, line=line))
+        out[name + "_frozen"] = g[fkey]
+    save("qary_harness", dict(runs=runs))
+
+
+def fx_qary_log(R, timing):
+    """use_log=True q-ary decodes (VectorDistributions/QaryMemorylessVectorDistribution.py:40,92-118:
+    logaddexp transforms, logsumexp normalisation, log-domain marginals): QSC received words and
+    random log-domain rows incl. -inf entries; info decisions and every leaf marginal."""
+    QMD, QPED, QMVD = R["QMD"], R["QPED"], R["QMVD"]
+    cls = QMVD.QaryMemorylessVectorDistribution
+    orig = cls.calcMarginalizedProbabilities
+    out, meta = {}, []
+    rs = np.random.default_rng(31)
+    for name, q, n, p, T in (("q4_n6", 4, 6, 0.11, 40), ("q3_n5", 3, 5, 0.2, 40), ("q2_n4", 2, 4, 0.11, 24)):
+        N = 1 << n
+        frozen = set(int(i) for i in rs.permutation(N)[:N // 2])
+        dec = QPED.QaryPolarEncoderDecoder(q, N, frozen, 1, use_log=True)
+        qsc = QMD.makeQSC(q, p)
+        xd = QMD.QaryMemorylessDistribution(q)
+        xd.probs = [qsc.calcXMarginals()]
+        xvd = xd.makeQaryMemorylessVectorDistribution(N, None, use_log=True)
+        y = rs.integers(0, q, size=(T, N))
+        xr = np.log(rs.random((T, N, q)))
+        xr[rs.random((T, N, q)) < 0.05] = -np.inf
+        xr[0, 0, :] = -np.inf
+        rows = [("chan", None), ("rand", xr)]
+        for kind, data in rows:
+            info = np.zeros((T, dec.k), np.uint8)
+            leaves = np.zeros((T, N, q))
+            xy_in = np.zeros((T, N, q))
+            for t in range(T):
+                if data is None:
+                    vd = qsc.makeQaryMemorylessVectorDistribution(N, [int(v) for v in y[t]], use_log=True)
+                else:
+                    vd = cls(q, N, use_log=True)
+                    vd.probs[:] = data[t]
+                xy_in[t] = vd.probs
+                rec = []
+
+                def wrapped(self, _rec=rec):
+                    m = orig(self)
+                    _rec.append(np.array(m, np.float64))
+                    return m
+                cls.calcMarginalizedProbabilities = wrapped
+                try:
+                    info[t] = dec.decode(xvd, vd)
+                finally:
+                    cls.calcMarginalizedProbabilities = orig
+                ii = [i for i in range(N) if i not in frozen]
+                assert len(rec) == len(ii)
+                for j, i in enumerate(ii):
+                    leaves[t, i] = rec[j]
+            out["%s_%s_xy" % (name, kind)] = xy_in
+            out["%s_%s_info" % (name, kind)] = info
+            out["%s_%s_leaf" % (name, kind)] = leaves
+        out[name + "_frozen"] = np.array([1 if i in frozen else 0 for i in range(N)], np.uint8)
+        meta.append(dict(name=name, q=q, n=n, p=p, trials=T))
+    save("qary_log", dict(sets=meta, note="leaf = log marginal at information leaves (0 elsewhere)"), **out)
+
+
 def _aux_groups(aux, n):
     """auxiliary (one set of input-letter indices per output letter) -> group[n], -1 = dropped"""
     g = np.full(n, -1, np.int64)
@@ -800,12 +1003,16 @@ FIXTURES = {
     "encode_binary": fx_encode,
     "qsc_q4_n256": fx_qsc,
     "harness_bsc_n64": fx_harness,
+    "harness_verbose": fx_harness_verbose,
     "deletion_n8": fx_deletion,
     "deletion_edge": fx_deletion_edge,
     "genie_bsc_n64": fx_genie_bsc,
     "main_deletion_n8": fx_main_deletion,
     "construct_bin": fx_construct_bin,
     "test2_run": fx_test2,
+    "construct_qary": fx_construct_qary,
+    "qary_harness": fx_qary_harness,
+    "qary_log": fx_qary_log,
 }
 
 

@@ -22,12 +22,13 @@ class HipError(RuntimeError):
 
 
 def lib():
-    """Load libpolarcub_hip.so (building it in-tree first if it is absent)."""
+    """Load libpolarcub_hip.so, (re)building it in-tree first when it is absent or does not
+    match the current sources (content-hash stamps, polarcub_amd/build.py)."""
     global _lib
     if _lib is not None:
         return _lib
     path = _build.LIB
-    if not os.path.exists(path):
+    if not os.path.exists(path) or not _build.up_to_date():
         _build.build()
     L = ctypes.CDLL(path)
     L.pcub_abi_version.restype = ctypes.c_int

@@ -3,12 +3,14 @@
     python -m polarcub_amd.build [--force]
 
 Compiles every csrc/*.hip translation unit to an object (in parallel, only the
-stale ones) and links polarcub_amd/lib/libpolarcub_hip.so with hipcc; builds the
+stale ones: staleness is a sha256 of the source, every header and the flags, stored
+beside each object and the library, never file mtimes) and links polarcub_amd/lib/libpolarcub_hip.so with hipcc; builds the
 host-only construction library polarcub_amd/lib/libpolarcub_construct.so
 (csrc/host/*.cpp) with g++.
 -ffp-contract=off is part of the arithmetic contract (no a*b+c contraction into
 FMA); never build with -ffast-math.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -35,10 +37,41 @@ CXX = os.environ.get("CXX", "g++")
 HOST_CFLAGS = ["-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-std=c++17", "-Wall", "-pthread"]
 
 
+def _digest(paths, extra=()):
+    """sha256 over the contents of `paths` (in order) and the strings in `extra` (flags)."""
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    for e in extra:
+        h.update(e.encode() + b"\0")
+    return h.hexdigest()
+
+
+def _stamp(target):
+    return target + ".sha256"
+
+
+def _stale(target, digest):
+    """A target is stale unless it exists and its stamp records the same content digest
+    (never decided by mtimes: a pushed tree can carry any mtimes)."""
+    if not os.path.exists(target) or not os.path.exists(_stamp(target)):
+        return True
+    with open(_stamp(target)) as f:
+        return f.read().strip() != digest
+
+
+def _write_stamp(target, digest):
+    with open(_stamp(target), "w") as f:
+        f.write(digest + "\n")
+
+
 def build_host(force=False, verbose=False):
     """The construction library: plain C++, IEEE binary64 without contraction, libm log2."""
     deps = HOST_SOURCES + [os.path.join(ROOT, "include", "polarcub_construct.h")]
-    if not force and not _stale(HOST_LIB, deps):
+    dig = _digest(deps, [CXX] + HOST_CFLAGS)
+    if not force and not _stale(HOST_LIB, dig):
         return HOST_LIB
     os.makedirs(LIBDIR, exist_ok=True)
     tmp = HOST_LIB + ".tmp"
@@ -47,32 +80,34 @@ def build_host(force=False, verbose=False):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, HOST_LIB)
+    _write_stamp(HOST_LIB, dig)
     return HOST_LIB
 
 
 def _headers():
     out = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     out.append(os.path.join(ROOT, "include", "polarcub_sc.h"))
-    return out
+    return sorted(out)
 
 
 def _obj(src):
     return os.path.join(OBJDIR, src.replace(".hip", ".o"))
 
 
-def _stale(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _obj_digest(src, hdr):
+    return _digest([os.path.join(CSRC, src)] + hdr, [HIPCC, ARCH] + CFLAGS)
+
+
+def _lib_digest(hdr):
+    return hashlib.sha256("".join(_obj_digest(s, hdr) for s in SOURCES).encode()).hexdigest()
 
 
 def up_to_date():
+    """True when every object and the library match the current sources, headers and flags."""
     hdr = _headers()
-    objs = [_obj(s) for s in SOURCES]
-    if any(_stale(_obj(s), hdr + [os.path.join(CSRC, s)]) for s in SOURCES):
+    if any(_stale(_obj(s), _obj_digest(s, hdr)) for s in SOURCES):
         return False
-    return not _stale(LIB, objs)
+    return not _stale(LIB, _lib_digest(hdr))
 
 
 def _compile(src, verbose):
@@ -84,6 +119,7 @@ def _compile(src, verbose):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, obj)
+    _write_stamp(obj, _obj_digest(src, _headers()))
 
 
 def build(force=False, verbose=False):
@@ -92,7 +128,8 @@ def build(force=False, verbose=False):
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)
     hdr = _headers()
-    todo = [s for s in SOURCES if force or _stale(_obj(s), hdr + [os.path.join(CSRC, s)])]
+    hdr_sorted = sorted(hdr)
+    todo = [s for s in SOURCES if force or _stale(_obj(s), _obj_digest(s, hdr_sorted))]
     with ThreadPoolExecutor(max(1, min(len(todo), int(os.environ.get("MAX_JOBS", "8"))))) as ex:
         list(ex.map(lambda s: _compile(s, verbose), todo))
     tmp = LIB + ".tmp"
@@ -101,6 +138,7 @@ def build(force=False, verbose=False):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    _write_stamp(LIB, _lib_digest(hdr_sorted))
     return LIB
 
 

@@ -330,7 +330,7 @@ def encodeDecodeSimulation(length, make_xVectorDistribution, make_codeword, simu
             if np.any(info_t != infos[t]):
                 errors += 1
                 if verbosity > 0:
-                    s = str(t0 + t) + ") error, transmitted inforamtion:\n" + str(list(infos[t]))
+                    s = str(t0 + t) + ") error, transmitted inforamtion:\n" + str(infos[t].tolist())
                     s += "\ndecoded information:\n" + str(info_t)
                     s += "\nencoded vector before guard bands added:\n" + str(encoded[t])
                     s += "\ncodeword:\n" + str(codeword)

@@ -141,32 +141,37 @@ class QaryPolarEncoderDecoder:
 def encodeDecodeSimulation(q, length, make_xVectorDistribution, make_codeword, simulateChannel,
                            make_xyVectorDistribution, numberOfTrials, frozenSet, commonRandomnessSeed=1,
                            randomInformationSeed=1, verbosity=0):
-    """q-ary Monte-Carlo SC run (QaryPolarEncoderDecoder.py:935-982), batched like the binary driver."""
+    """q-ary Monte-Carlo SC run (QaryPolarEncoderDecoder.py:935-982), batched like the binary driver:
+    trials in chunks of 2^14 (information from the seeded stream in trial order, the user's
+    closures once per trial in trial order, one GPU encode and one GPU decode per chunk)."""
     xvd = make_xVectorDistribution()
     encDec = QaryPolarEncoderDecoder(q, length, frozenSet, commonRandomnessSeed)
     rng = random.Random(randomInformationSeed)
     errors = 0
-    infos = [rng.choices(range(0, q), k=encDec.k) for _ in range(numberOfTrials)]
-    if encDec._device_ok() and numberOfTrials:
-        encoded = encDec.encode_batch(np.array(infos, dtype=np.int64).reshape(numberOfTrials, encDec.k))
-    else:
-        encoded = [encDec.encode(xvd, inf) for inf in infos]
-    batch, slots = [], []
-    decoded = [None] * numberOfTrials
-    for t in range(numberOfTrials):
-        xyvd = make_xyVectorDistribution(simulateChannel(make_codeword(encoded[t])))
-        if encDec._device_ok() and _is_qary_memoryless(xyvd) and not getattr(xyvd, "use_log", False):
-            batch.append(np.asarray(xyvd.probs, dtype=np.float64))
-            slots.append(t)
+    chunk = 1 << 14
+    for t0 in range(0, numberOfTrials, chunk):
+        T = min(chunk, numberOfTrials - t0)
+        infos = [rng.choices(range(0, q), k=encDec.k) for _ in range(T)]
+        if encDec._device_ok():
+            encoded = encDec.encode_batch(np.array(infos, dtype=np.int64).reshape(T, encDec.k))
         else:
-            decoded[t] = encDec.decode(xvd, xyvd)
-    if batch:
-        dec = encDec.decode_batch(np.stack(batch))
-        for i, t in enumerate(slots):
-            decoded[t] = dec[i]
-    for t in range(numberOfTrials):
-        if not np.array_equal(infos[t], decoded[t]):
-            errors += 1
+            encoded = [encDec.encode(xvd, inf) for inf in infos]
+        batch, slots = [], []
+        decoded = [None] * T
+        for t in range(T):
+            xyvd = make_xyVectorDistribution(simulateChannel(make_codeword(encoded[t])))
+            if encDec._device_ok() and _is_qary_memoryless(xyvd) and not getattr(xyvd, "use_log", False):
+                batch.append(np.asarray(xyvd.probs, dtype=np.float64))
+                slots.append(t)
+            else:
+                decoded[t] = encDec.decode(xvd, xyvd)
+        if batch:
+            dec = encDec.decode_batch(np.stack(batch))
+            for i, t in enumerate(slots):
+                decoded[t] = dec[i]
+        for t in range(T):
+            if not np.array_equal(infos[t], decoded[t]):
+                errors += 1
     print("Error probability = ", errors, "/", numberOfTrials, " = ", errors / numberOfTrials)
 
 

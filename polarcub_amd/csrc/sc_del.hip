@@ -390,6 +390,7 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     A.leaf = leaf;
     const long long cpb = kBlock >> (n - n0);
     const long long grid = (B + cpb - 1) / cpb;
+    if (grid * kBlock > 0xffffffffLL) return PCUB_EINVAL;  // 32-bit dispatch grid (work-items)
     // bit-packed received words in LDS when the group's words fit in 32 KiB (always for
     // the 64-trellis shapes; very long padded rows of small codes parse from HBM)
     const long long rw = ((long long)stride + 31) / 32;

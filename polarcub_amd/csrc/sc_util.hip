@@ -17,6 +17,8 @@ using namespace pcub;
 namespace {
 
 constexpr int kEncBlock = 64;
+constexpr int kEncLdsMaxLog2N = 14;  // W * kEncBlock * 4 B of LDS: 128 KiB at n = 14
+constexpr int kMaxLog2N = 24;        // the decoder's bound (pcub_sc_decode_bin)
 
 __global__ __launch_bounds__(kEncBlock) void k_encode_bin(const uint32_t* __restrict__ info, long long B, int n,
                                                           const uint32_t* __restrict__ fmask,
@@ -66,6 +68,52 @@ __global__ __launch_bounds__(kEncBlock) void k_encode_bin(const uint32_t* __rest
         for (int t = 0; t < tb; ++t) {
             const uint32_t p = bitrev((uint32_t)(32 * w + t), n);
             o |= ((u[(p >> 5) * kEncBlock] >> (p & 31u)) & 1u) << t;
+        }
+        x[(long long)w * B + cw] = o;
+    }
+}
+
+// Long codes (n > 14: the 64-codeword LDS tile would exceed the LDS): the same three
+// phases with u in a global scratch column per codeword ([W][B] words, coalesced across
+// the lanes of a wave), then x = bitrev_N(F u) gathered from it.
+__global__ __launch_bounds__(256) void k_encode_bin_global(const uint32_t* __restrict__ info, long long B, int n,
+                                                           const uint32_t* __restrict__ fmask,
+                                                           const uint32_t* __restrict__ fval,
+                                                           uint32_t* __restrict__ u, uint32_t* __restrict__ x) {
+    const int N = 1 << n;
+    const int W = N / 32;
+    const long long cw = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cw >= B) return;
+    int iw = 0, ileft = 0;
+    uint32_t ibuf = 0;
+    for (int w = 0; w < W; ++w) {
+        const uint32_t fm = fmask[w], fv = fval[w];
+        uint32_t uw = fv & fm;
+        for (uint32_t m = ~fm; m != 0u; m &= m - 1u) {
+            if (ileft == 0) {
+                ibuf = info[(long long)iw * B + cw];
+                ++iw;
+                ileft = 32;
+            }
+            uw |= (ibuf & 1u) << __builtin_ctz(m);
+            ibuf >>= 1;
+            --ileft;
+        }
+        uw ^= (uw >> 1) & 0x55555555u;
+        uw ^= (uw >> 2) & 0x33333333u;
+        uw ^= (uw >> 4) & 0x0f0f0f0fu;
+        uw ^= (uw >> 8) & 0x00ff00ffu;
+        uw ^= (uw >> 16) & 0x0000ffffu;
+        u[(long long)w * B + cw] = uw;
+    }
+    for (int hw = 1; hw < W; hw <<= 1)
+        for (int b0 = 0; b0 < W; b0 += 2 * hw)
+            for (int i = 0; i < hw; ++i) u[(long long)(b0 + i) * B + cw] ^= u[(long long)(b0 + hw + i) * B + cw];
+    for (int w = 0; w < W; ++w) {
+        uint32_t o = 0;
+        for (int t = 0; t < 32; ++t) {
+            const uint32_t p = bitrev((uint32_t)(32 * w + t), n);
+            o |= ((u[(long long)(p >> 5) * B + cw] >> (p & 31u)) & 1u) << t;
         }
         x[(long long)w * B + cw] = o;
     }
@@ -135,10 +183,22 @@ __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ sr
 
 extern "C" int pcub_polar_encode_bin(const uint32_t* info_words, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
                                      const uint32_t* frozen_val, int32_t K, uint32_t* x_words, void* stream) {
-    if (B < 0 || log2N < 0 || log2N > 14 || !frozen_mask || !frozen_val || !x_words) return PCUB_EINVAL;
+    if (B < 0 || log2N < 0 || log2N > kMaxLog2N || !frozen_mask || !frozen_val || !x_words) return PCUB_EINVAL;
     if (K < 0 || K > (1 << log2N) || (K > 0 && !info_words)) return PCUB_EINVAL;
     if (B == 0) return 0;
     const int W = log2N >= 5 ? (1 << (log2N - 5)) : 1;
+    if (log2N > kEncLdsMaxLog2N) {
+        if ((B + 255) / 256 > 0x7fffffffLL) return PCUB_EINVAL;
+        uint32_t* u = nullptr;
+        hipError_t e = hipMallocAsync((void**)&u, (size_t)W * (size_t)B * sizeof(uint32_t), (hipStream_t)stream);
+        if (e != hipSuccess) return (int)e;
+        hipLaunchKernelGGL(k_encode_bin_global, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           info_words, (long long)B, log2N, frozen_mask, frozen_val, u, x_words);
+        e = hipGetLastError();
+        const hipError_t f = hipFreeAsync(u, (hipStream_t)stream);
+        return (int)(e != hipSuccess ? e : f);
+    }
+    if ((B + kEncBlock - 1) / kEncBlock > 0x7fffffffLL) return PCUB_EINVAL;
     const size_t lds = (size_t)W * kEncBlock * sizeof(uint32_t);
     hipLaunchKernelGGL(k_encode_bin, dim3((unsigned)((B + kEncBlock - 1) / kEncBlock)), dim3(kEncBlock), lds,
                        (hipStream_t)stream, info_words, (long long)B, log2N, frozen_mask, frozen_val, K, x_words);
@@ -166,6 +226,8 @@ extern "C" int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits,
 extern "C" int pcub_transpose_pairs(const double* src, int64_t B, int32_t N, int32_t q, double* dst, void* stream) {
     if (B < 0 || N < 0 || q < 1 || q > 8 || (B > 0 && N > 0 && (!src || !dst))) return PCUB_EINVAL;
     if (B == 0 || N == 0) return 0;
+    // 32-bit dispatch grid: x extent in work-items = 256 * ceil(B / 32)
+    if (((B + 31) / 32) * 256 > 0xffffffffLL || ((N + 15) / 16) > 65535) return PCUB_EINVAL;
     const dim3 grid((unsigned)((B + 31) / 32), (unsigned)((N + 15) / 16));
     hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, (hipStream_t)stream, src, (long long)B, N, q, dst);
     return (int)hipGetLastError();

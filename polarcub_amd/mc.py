@@ -36,6 +36,24 @@ def shard_range(total, rank, world):
     return lo, hi
 
 
+def rank_offset(rank, batch):
+    """First global codeword index of rank r under weak scaling (every rank owns `batch`
+    codewords: [r*batch, (r+1)*batch)); the Philox streams are keyed by this index, so the
+    union over ranks is the single-process run over [0, world*batch)."""
+    return int(rank) * int(batch)
+
+
+def gather_floats(values, device=None):
+    """all_gather of one small float vector per rank -> [world][len] list (identity when not
+    distributed)."""
+    v = torch.tensor([float(x) for x in values], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        out = [torch.empty_like(v) for _ in range(dist.get_world_size())]
+        dist.all_gather(out, v)
+        return [o.tolist() for o in out]
+    return [v.tolist()]
+
+
 def reduce_counters(counters, elapsed, device=None):
     """Sum the int64 counters and max the elapsed time over all ranks (no-op when not
     distributed).  device: where the collective's tensors live (a CUDA device for RCCL,

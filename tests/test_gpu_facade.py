@@ -81,3 +81,68 @@ def test_encode_decode_simulation_prints_reference_line():
     with contextlib.redirect_stdout(buf):
         coding.encodeDecodeSimulation(N, make_x, lambda e: e, channel, make_xy, m["trials"], fs)
     assert buf.getvalue().strip().splitlines()[-1] == m["line"]
+
+
+def test_encode_decode_simulation_verbose_printout():
+    """verbosity=1 error printout (BinaryPolarEncoderDecoder.py:374-385) line for line."""
+    from polarcub_amd import coding, scalar
+    g = load_golden("harness_verbose")
+    m = g["meta"]
+    N = m["N"]
+    fs = set(int(i) for i in np.nonzero(g["frozen"])[0])
+    xy_dist = scalar.makeBSC(m["p"])
+
+    def make_x():
+        xd = scalar.BinaryMemorylessDistribution()
+        xd.probs.append([xy_dist.calcXMarginal(0), xy_dist.calcXMarginal(1)])
+        return xd.makeBinaryMemorylessVectorDistribution(N, None)
+
+    def channel(codeword):
+        out = []
+        for x in codeword:
+            rnd = random.random()
+            s = 0.0
+            for y in range(len(xy_dist.probs)):
+                if s + xy_dist.probXGivenY(x, y) >= rnd:
+                    out.append(y)
+                    break
+                s += xy_dist.probXGivenY(x, y)
+        return out
+
+    def make_xy(received):
+        return xy_dist.makeBinaryMemorylessVectorDistribution(len(received), received)
+
+    random.seed(m["global_seed"])
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        coding.encodeDecodeSimulation(N, make_x, lambda e: e, channel, make_xy, m["trials"], fs, verbosity=1)
+    assert buf.getvalue() == m["stdout"]
+
+
+@pytest.mark.parametrize("n", [15, 16])
+def test_long_code_encode_matches_oracle(n):
+    """Codes past the encoder's LDS tile (n > 14) take the global-scratch encoder: the
+    facade's encode and the device Monte-Carlo pipeline accept them."""
+    import torch
+
+    from oracle import orc
+    from polarcub_amd import coding, mc, sc, vectors
+    N = 1 << n
+    rng = np.random.default_rng(n)
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    fs = set(int(i) for i in np.nonzero(frozen)[0])
+    enc = coding.BinaryPolarEncoderDecoder(N, fs, 3)
+    xvd = vectors.BinaryMemorylessVectorDistribution(N)
+    xvd.probs[:] = 0.5
+    fval = np.where(0.5 >= enc.randomlyGeneratedNumbers, 0, 1).astype(np.uint8)
+    infos = rng.integers(0, 2, size=(3, enc.k)).astype(np.uint8)
+    for b in range(3):
+        x = enc.encode(xvd, list(infos[b]))
+        assert np.array_equal(x, orc.encode_bin(infos[b], frozen, fval=fval))
+    X = enc.encode_batch(infos)
+    for b in range(3):
+        assert np.array_equal(X[b], orc.encode_bin(infos[b], frozen, fval=fval))
+    code = sc.CodeSpec(N, frozen, fval, device="cuda:0")
+    cnt = mc.run_bin(code, 5, 0, 96, mc.CHANNEL_BSC, 0.0, chunk=64)  # noiseless: every word decodes
+    torch.cuda.synchronize()
+    assert cnt[0] == 96 and cnt[1] == 0 and cnt[2] == 0

@@ -274,10 +274,19 @@ class Qary:
         self.N = 1 << self.n
         self.K = self.N // 2
         self.B = a.batch
-        z = construction.bhattacharyya_z(self.n, 0.5)
-        order = sorted(range(self.N), key=lambda i: (z[i], i))
-        mask = np.ones(self.N, np.uint8)
-        mask[order[:self.K]] = 0
+        if self.q == 4 and self.n == 8 and abs(a.qsc_p - 0.11) < 1e-12:
+            # the reference's own q-ary degrading construction (n=8, L=64, QSC(0.11),
+            # numInfoIndices=127 -> K=128), a fixture made by running it (oracle/make_golden.py)
+            g = np.load(os.path.join(ROOT, "tests", "golden", "construct_qary.npz"), allow_pickle=False)
+            mask = g["qsc4_n8_L64_frozen"].astype(np.uint8)
+            self.construction = "reference QaryMemorylessDistribution degrading construction, L=64, numInfoIndices=127"
+        else:
+            z = construction.bhattacharyya_z(self.n, 0.5)
+            order = sorted(range(self.N), key=lambda i: (z[i], i))
+            mask = np.ones(self.N, np.uint8)
+            mask[order[:self.K]] = 0
+            self.construction = "binary Bhattacharyya ranking (stand-in)"
+        self.K = int(self.N - mask.sum())
         self.code = sc.QaryCode(self.q, self.N, mask, device=device)
         if a.qlanes:
             sc.set_qary_lanes(a.qlanes)
@@ -309,7 +318,7 @@ class Qary:
             data="synthetic: uniform info symbols, GPU q-ary encoder, QSC(%.2f) on device" % self.a.qsc_p,
             config={"workload": "q-ary SC decode q=%d N=%d K=%d QSC(%.2f) (BASELINE configs[3])"
                                 % (self.q, self.N, self.K, self.a.qsc_p),
-                    "N": self.N, "K": self.K, "q": self.q, "batch_per_gpu": self.B,
+                    "N": self.N, "K": self.K, "q": self.q, "batch_per_gpu": self.B, "frozen_set": self.construction,
                     "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
 
     def cpu_baseline(self, seconds=10.0):

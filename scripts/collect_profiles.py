@@ -32,6 +32,19 @@ def read_csv(path):
         return list(csv.DictReader(f))
 
 
+def grid_of(r):
+    """Grid size in work-items (kernel trace: Grid_Size_X*Y*Z; PMC rows: Grid_Size)."""
+    if "Grid_Size" in r:
+        return int(r["Grid_Size"])
+    return int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) * int(r.get("Grid_Size_Z", 1) or 1)
+
+
+def wg_of(r):
+    if "Workgroup_Size" in r:
+        return int(r["Workgroup_Size"])
+    return int(r["Workgroup_Size_X"]) * int(r.get("Workgroup_Size_Y", 1) or 1) * int(r.get("Workgroup_Size_Z", 1) or 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", default="r2")
@@ -57,8 +70,8 @@ def main():
     if traces:
         rows = [r for r in read_csv(traces[0]) if a.kernel in r["Kernel_Name"]]
         if grid is None and rows:
-            grid = collections.Counter(int(r["Grid_Size"]) for r in rows).most_common(1)[0][0]
-        sel = [r for r in rows if int(r["Grid_Size"]) == grid]
+            grid = collections.Counter(grid_of(r) for r in rows).most_common(1)[0][0]
+        sel = [r for r in rows if grid_of(r) == grid]
         with open(os.path.join(dst, "kernel_trace.csv"), "w", newline="") as f:
             w = csv.DictWriter(f, fieldnames=list(rows[0].keys()) if rows else ["none"])
             w.writeheader()
@@ -67,7 +80,7 @@ def main():
             durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in sel]
             summ.update(trace_calls=len(sel), trace_avg_ms=sum(durs) / len(durs), trace_min_ms=min(durs),
                         trace_max_ms=max(durs), trace_kernel_name=sel[0]["Kernel_Name"], grid_size=grid,
-                        workgroup_size=int(sel[0]["Workgroup_Size"]), vgpr=int(sel[0].get("VGPR_Count", 0) or 0),
+                        workgroup_size=wg_of(sel[0]), vgpr=int(sel[0].get("VGPR_Count", 0) or 0),
                         sgpr=int(sel[0].get("SGPR_Count", 0) or 0),
                         scratch_bytes_per_lane=int(sel[0].get("Scratch_Size", 0) or 0),
                         lds_bytes=int(sel[0].get("LDS_Block_Size", 0) or 0),
@@ -82,8 +95,8 @@ def main():
             rs = [r for r in read_csv(p) if a.kernel in r["Kernel_Name"]]
             if not rs:
                 continue
-            g = grid if grid is not None else collections.Counter(int(r["Grid_Size"]) for r in rs).most_common(1)[0][0]
-            rs = [r for r in rs if int(r["Grid_Size"]) == g]
+            g = grid if grid is not None else collections.Counter(grid_of(r) for r in rs).most_common(1)[0][0]
+            rs = [r for r in rs if grid_of(r) == g]
             with open(os.path.join(dst, os.path.basename(d) + ".csv"), "w", newline="") as f:
                 w = csv.DictWriter(f, fieldnames=list(rs[0].keys()))
                 w.writeheader()

@@ -290,6 +290,9 @@ class Qary:
         self.code = sc.QaryCode(self.q, self.N, mask, device=device)
         if a.qlanes:
             sc.set_qary_lanes(a.qlanes)
+        if a.qregs:
+            sc.set_qary_regs(a.qregs)
+
         self.dec = sc.QaryDecoder(self.code)
         gen = torch.Generator(device=device)
         gen.manual_seed(mc.shard_seed(a.seed, rank))
@@ -435,6 +438,7 @@ def build_parser():
     ap.add_argument("--q", type=int, default=4)
     ap.add_argument("--qsc-p", type=float, default=0.11)
     ap.add_argument("--qlanes", type=int, default=0, help="q-ary: lanes per codeword (0 = the library's)")
+    ap.add_argument("--qregs", type=int, default=0, help="q-ary: cap on register positions per lane (0 = the library's)")
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU")
     ap.add_argument("--variant", type=int, default=None, help="binary decode kernel variant (default: the library's)")
     ap.add_argument("--max-blocks", type=int, default=0, help="cap decode workgroups per CU (0 = occupancy)")

@@ -924,7 +924,7 @@ def fx_qary_harness(R, timing):
         print("  reference q-ary printed:", line)
         runs.append(dict(name=name, q=q, n=n, p=p, trials=T, global_seed=seed, frozen_key=fkey, line=line))
         out[name + "_frozen"] = g[fkey]
-    save("qary_harness", dict(runs=runs))
+    save("qary_harness", dict(runs=runs), **out)
 
 
 def fx_qary_log(R, timing):

@@ -12,34 +12,19 @@
 //   combine x[2h] = (xm+xp)%q, x[2h+1] = (q-xp)%q                                    (:397-399)
 // The per-codeword schedule (register subtrees, fused chain passes, rate-0
 // skipping, G lanes per codeword) is in sc_qary_body.h; this file owns the
-// launch geometry: G lanes per codeword (default 2, fewer for short codes),
+// launch geometry: G lanes per codeword (default 4, fewer for short codes),
 // 256-thread workgroups, a resident grid striding over 256/G-codeword tiles so
 // the per-slot stage buffers are reused.
 #include <hip/hip_runtime.h>
 
 #include "polarcub_sc.h"
-#include "sc_qary_body.h"
+#include "sc_qary_kern.h"
 
 using namespace pcub;
 
 namespace {
 
-constexpr int kQBlock = 256;
-constexpr int kQWaves = 3;  // waves per SIMD the register allocation must allow (3 workgroups per CU)
-
-template <int Q, int S, int G>
-__global__ __launch_bounds__(kQBlock, kQWaves) void k_sc_qary(QArgs A) {
-    constexpr int CWB = kQBlock / G;  // codewords per tile
-    const long long slot = (long long)blockIdx.x * kQBlock + threadIdx.x;
-    const int j = threadIdx.x & (G - 1);
-    const int lane = threadIdx.x & 63;
-    const long long ntiles = (A.B + CWB - 1) / CWB;
-    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const long long cw = t * CWB + threadIdx.x / G;
-        const bool valid = cw < A.B;
-        decode_qary_cw<Q, S, G>(A, valid ? cw : A.B - 1, slot, valid, j, lane);
-    }
-}
+constexpr int kQBlock = kQaryBlock;
 
 // rate-0 table: frozen bytes -> words -> first all-frozen depth per register subtree
 __global__ __launch_bounds__(kQBlock) void k_q_frozen_words(const uint8_t* frozen, int N, uint32_t* words) {
@@ -83,9 +68,8 @@ __global__ __launch_bounds__(kQBlock) void k_encode_qary(const uint8_t* info, lo
     }
 }
 
-typedef void (*QKern)(QArgs);
-
-int g_qlanes = 2;  // requested lanes per codeword (pcub_sc_set_qary_lanes): 2 is the fastest at q=4 N=256
+int g_qlanes = 4;  // requested lanes per codeword (pcub_sc_set_qary_lanes)
+int g_qregs = 0;   // cap on register positions per lane (pcub_sc_set_qary_regs; 0 = the default)
 
 // register positions per lane S and lanes per codeword G for a code of 2^n:
 // S = 8 (q <= 4) or 4, G = the requested lanes, both reduced until N >= 2*S*G
@@ -93,58 +77,31 @@ struct QGeom {
     int S, G;
 };
 QGeom q_geom(int q, int n) {
-    QGeom c{q <= 4 ? 8 : 4, g_qlanes};
+    QGeom c{4, g_qlanes};  // 8 register positions (q <= 4) via pcub_sc_set_qary_regs
+    if (g_qregs > 0) c.S = (q <= 4 || g_qregs <= 4) ? g_qregs : 4;
     while (c.G > 1 && (1 << n) < 2 * c.S * c.G) c.G >>= 1;
     while (c.S > 1 && (1 << n) < 2 * c.S * c.G) c.S >>= 1;
     return c;
 }
 
-template <int Q, int G>
-QKern qkernel_s(int S) {
-    switch (S) {
-        case 1: return k_sc_qary<Q, 1, G>;
-        case 2: return k_sc_qary<Q, 2, G>;
-        case 4: return k_sc_qary<Q, 4, G>;
-        case 8:
-            if constexpr (Q <= 4) return k_sc_qary<Q, 8, G>;
-            else return nullptr;
-        default: return nullptr;
-    }
-}
-
-template <int Q>
-QKern qkernel_g(QGeom c) {
-    switch (c.G) {
-        case 1: return qkernel_s<Q, 1>(c.S);
-        case 2: return qkernel_s<Q, 2>(c.S);
-        case 4: return qkernel_s<Q, 4>(c.S);
-        default: return nullptr;
-    }
-}
-
-QKern qkernel(int q, int n) {
+QKern qkernel(int q, int n, int* waves = nullptr) {
     const QGeom c = q_geom(q, n);
-    switch (q) {
-        case 2: return qkernel_g<2>(c);
-        case 3: return qkernel_g<3>(c);
-        case 4: return qkernel_g<4>(c);
-        case 5: return qkernel_g<5>(c);
-        case 6: return qkernel_g<6>(c);
-        case 7: return qkernel_g<7>(c);
-        case 8: return qkernel_g<8>(c);
-        default: return nullptr;
-    }
+    if (waves) *waves = qary_waves(q, c.S);
+    return qary_kernel(q, c.S, c.G);
 }
 
 long long qgrid(long long B, int q, int n) {
     int dev = 0, cus = 0, occ = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, qkernel(q, n), kQBlock, 0) != hipSuccess || occ < 1) occ = 1;
-    // the launch bounds guarantee kQWaves resident workgroups per CU (the occupancy
-    // query reports 1 for these kernels on ROCm 7.2)
-    if (occ < kQWaves) occ = kQWaves;
-    const long long cwb = kQBlock / q_geom(q, n).G;
+    int waves = 1;
+    const QKern kern = qkernel(q, n, &waves);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kQBlock, 0) != hipSuccess || occ < 1) occ = 1;
+    // the launch bounds guarantee `waves` resident workgroups per CU (the occupancy
+    // query under-reports these kernels on ROCm 7.2)
+    const QGeom cg = q_geom(q, n);
+    if (occ < waves) occ = waves;
+    const long long cwb = kQBlock / cg.G;
     const long long ntiles = (B + cwb - 1) / cwb;
     const long long g = (long long)cus * occ;
     return ntiles < g ? ntiles : g;
@@ -201,7 +158,7 @@ extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, i
     A.xy = xy;
     A.B = B;
     A.n = log2N;
-    A.frozen = frozen;
+    A.fwords = words;
     A.ef = ef;
     A.info = info;
     A.xhat = xhat;
@@ -229,5 +186,15 @@ extern "C" int pcub_sc_set_qary_lanes(int G) {
     if (G != 1 && G != 2 && G != 4) return PCUB_EINVAL;
     const int old = g_qlanes;
     g_qlanes = G;
+    return old;
+}
+
+// Tuning hook (not part of the stable ABI): cap on the register positions per lane of
+// the q-ary decode kernel (0 = default: 8 for q <= 4, else 4; otherwise 2 or 4).
+// Returns the previous value.
+extern "C" int pcub_sc_set_qary_regs(int S) {
+    if (S != 0 && S != 2 && S != 4 && S != 8) return PCUB_EINVAL;
+    const int old = g_qregs;
+    g_qregs = S;
     return old;
 }

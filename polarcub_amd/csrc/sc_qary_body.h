@@ -10,26 +10,32 @@
 //   leaf   s = sum as above; m = p/s (or 1/q); u = first argmax(m)                  (:69-90, :342)
 //   frozen symbols are 0 (:347-351); the a-priori tree is never consulted.
 //   combine x[2h] = (xm+xp)%q, x[2h+1] = (q-xp)%q                                    (:397-399)
+// Every quotient p/t is the correctly rounded one (q_div: one IEEE division for
+// RN(1/t) per vector, then Markstein's correction per component, inside a guarded
+// range; plain division outside it).
 //
-// Schedule (as the binary kernel, sc_bin_body.h, with one codeword per lane):
-// half-split order inside every node; the bottom S positions of every chain live
-// in registers (QSub<S>); stage levels 1..D-1 in a per-slot scratch (q doubles
-// per position as ceil(q/2) 16-byte pairs, slot-minor, so a wave's access is one
-// contiguous 1 KiB); the re-encoded symbols one byte each, four to a 32-bit word
-// (combined word-wise, see q_combine_words).  A chain -- one plus transform, then minus transforms
-// down to depth D -- is evaluated in passes of up to two fused levels per column,
-// so a level written inside a pass is consumed from registers by the next one.
-// Nodes whose u range is entirely frozen are never evaluated (their symbols are 0
-// and so is their re-encoding), driven by the per-code rate-0 depth table `ef`.
+// Schedule (as the binary kernel, sc_bin_body.h): half-split order inside every
+// node; G lanes per codeword, lane j owning positions p = j (mod G) of every node
+// of length >= G, so every butterfly of a node of length >= 2G is lane-local and
+// each lane runs the one-lane schedule on a virtual tree of N/G positions; a
+// virtual leaf is a real node of G positions, one per lane, finished by QXSub<G>
+// with cross-lane exchanges.  The bottom S virtual positions of every chain live
+// in registers (QSub<S>); stage levels 1..D-1 in a per-slot scratch (q doubles per
+// position as ceil(q/2) 16-byte pairs, slot-minor, so a wave's access is one
+// contiguous run); re-encoded symbols one byte each, four to a 32-bit word.
 //
-// G lanes per codeword (G = 1, 2, 4), as in the binary kernel: lane j owns the
-// positions p = j (mod G) of every node of length >= G, so every butterfly of a
-// node of length >= 2G is lane-local and each lane runs the G = 1 schedule on a
-// virtual tree of N/G positions; a virtual leaf is a real node of G positions,
-// one per lane, finished by QXSub<G> with cross-lane exchanges.  More lanes per
-// codeword = fewer stage levels in memory (the kernel is bound by their traffic).
+// Traffic.  Register subtree k is reached by a chain: one plus transform from
+// depth d0-1 (minus for k = 0), then minus transforms down to depth D.  A chain
+// is evaluated in passes of up to three fused levels, each column depth-first
+// (QCol), every level of the pass stored once for the plus transforms to come and
+// consumed from registers by the next level; the last pass lands in registers.
+// So a stored node is written once and read once (by its plus child's chain),
+// except the source of a pass after the first (an extra read, 1/8 of the first
+// pass's source).  Nodes whose u range is entirely frozen are never evaluated
+// (their symbols are 0 and so is their re-encoding), driven by the per-code
+// rate-0 depth table `ef`.
 #pragma once
-#include "sc_bin_body.h"  // first_frozen_depth, launder
+#include "sc_bin_body.h"  // first_frozen_depth, launder, xor_shfl_c, ld2/st2
 #include "sc_common.h"
 
 namespace pcub {
@@ -39,15 +45,41 @@ struct QV {
     double p[Q];
 };
 
+PCUB_HD double fma_d(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+// v[x] / t for every component, each the correctly rounded quotient the
+// reference's `p[x] /= t` produces.  Fast path: y = RN(1/t) by one IEEE division,
+// then per component q0 = RN(p*y) (within an ulp of p/t), r = p - q0*t (exact by
+// fma) and RN(q0 + r*y) = RN(p/t) (Markstein).  The guard keeps t, y and every
+// quotient far from underflow/overflow (t in [2^-200, 2^200], p = 0 or
+// p >= t * 2^-800), where those steps are exact; outside it, plain division.
+// tests/emu checks the fast path against division over random and edge inputs.
+template <int Q>
+PCUB_HD void q_div(QV<Q>& v, double t) {
+    const double lo = t * 0x1p-800;
+    bool fast = t >= 0x1p-200 && t <= 0x1p+200;
+#pragma unroll
+    for (int x = 0; x < Q; ++x) fast = fast && (v.p[x] == 0.0 || v.p[x] >= lo);
+    if (fast) {
+        const double y = 1.0 / t;
+#pragma unroll
+        for (int x = 0; x < Q; ++x) {
+            const double q0 = v.p[x] * y;
+            const double r = fma_d(-q0, t, v.p[x]);
+            v.p[x] = fma_d(r, y, q0);
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < Q; ++x) v.p[x] = v.p[x] / t;
+    }
+}
+
 template <int Q>
 PCUB_HD QV<Q> q_normalize(QV<Q> v) {
     double t = 0.0;
 #pragma unroll
     for (int x = 0; x < Q; ++x) t = t + v.p[x];
-    if (t != 0.0) {
-#pragma unroll
-        for (int x = 0; x < Q; ++x) v.p[x] = v.p[x] / t;
-    }
+    if (t != 0.0) q_div<Q>(v, t);
     return v;
 }
 
@@ -68,31 +100,36 @@ PCUB_HD QV<Q> q_minus(const QV<Q>& a, const QV<Q>& b) {
 
 template <int Q>
 PCUB_HD QV<Q> q_plus(const QV<Q>& a, const QV<Q>& b, int u1) {
+    // r[u2] = a[(u1+u2)%Q] with a lane-divergent u1: rotate by each set bit of u1
+    // (ceil(log2 Q) rounds of Q selects) instead of selecting every element
+    QV<Q> r = a;
+#pragma unroll
+    for (int sh = 1; sh < Q; sh <<= 1) {
+        const bool on = (u1 & sh) != 0;
+        QV<Q> t;
+#pragma unroll
+        for (int i = 0; i < Q; ++i) t.p[i] = on ? r.p[(i + sh) % Q] : r.p[i];
+        r = t;
+    }
     QV<Q> o;
 #pragma unroll
-    for (int u2 = 0; u2 < Q; ++u2) {
-        // a[(u1+u2)%Q] with a lane-divergent u1: select instead of indexing
-        const int x1 = (u1 + u2) % Q;
-        double ax = a.p[0];
-#pragma unroll
-        for (int x = 1; x < Q; ++x) ax = (x1 == x) ? a.p[x] : ax;
-        o.p[u2] = 0.0 + ax * b.p[(Q - u2) % Q];
-    }
+    for (int u2 = 0; u2 < Q; ++u2) o.p[u2] = 0.0 + r.p[u2] * b.p[(Q - u2) % Q];
     return q_normalize<Q>(o);
 }
 
 template <int Q>
-PCUB_HD int q_leaf(const QV<Q>& v) {
+PCUB_HD int q_leaf(QV<Q> v) {
     double s = 0.0;
 #pragma unroll
     for (int x = 0; x < Q; ++x) s = s + v.p[x];
+    if (!(s > 0.0)) return 0;  // every marginal 1/q: the first index
+    q_div<Q>(v, s);
     int arg = 0;
-    double best = 0.0;
+    double best = v.p[0];
 #pragma unroll
-    for (int x = 0; x < Q; ++x) {
-        const double m = (s > 0.0) ? v.p[x] / s : 1.0 / (double)Q;
-        if (x == 0 || m > best) {
-            best = m;
+    for (int x = 1; x < Q; ++x) {
+        if (v.p[x] > best) {
+            best = v.p[x];
             arg = x;
         }
     }
@@ -100,15 +137,15 @@ PCUB_HD int q_leaf(const QV<Q>& v) {
 }
 
 struct QArgs {
-    const double* xy;       // [N][B][Q]
+    const double* xy;        // [N][B][Q]
     long long B;
     int n;
-    const uint8_t* frozen;  // [N] 0/1
-    const uint8_t* ef;      // [2^D] first rate-0 depth on each register subtree's chain
-    uint8_t* info;          // [K][B]
-    uint8_t* xhat;          // [N][B] or null
-    double2* scratch;       // [(N - 2S) positions][ceil(Q/2)][nslots]
-    uint32_t* ysym;         // [N/4 words][nslots], symbol of position p in byte p % 4 of word p / 4
+    const uint32_t* fwords;  // [ceil(N/32)] frozen mask, bit i = position i
+    const uint8_t* ef;       // [2^D] first rate-0 depth on each register subtree's chain
+    uint8_t* info;           // [K][B]
+    uint8_t* xhat;           // [N][B] or null
+    double2* scratch;        // [(N/G - 2S) positions][ceil(Q/2)][nslots]
+    uint32_t* ysym;          // [N/G/4 words][nslots], symbol of position p in byte p % 4 of word p / 4
     long long nslots;
 };
 
@@ -130,22 +167,26 @@ PCUB_HD void q_combine_words(uint32_t& m, uint32_t& p) {
 }
 
 PCUB_HD int q_sym(const uint32_t* Y, long long ns, int pos) {
-    return (int)((Y[(long long)(pos >> 2) * ns] >> ((pos & 3) * 8)) & 0xffu);
+    return (int)((ldu(Y + (long long)(pos >> 2) * ns) >> ((pos & 3) * 8)) & 0xffu);
 }
 
 // Decisions of the register subtree: information symbols go out in u order
-// (identical in the G lanes of a codeword; lane w % G stores row w).
+// (identical in the G lanes of a codeword; lane w % G stores row w).  Plain
+// fields, no pointer to the kernel argument (that would put it in scratch).
 struct QInfo {
-    const QArgs* A;
+    uint8_t* info;
+    long long B;
     long long cw;
     bool store;
     int w;     // next information row
     int j;     // lane of the codeword
     int gm;    // G - 1
+    uint32_t fm;  // frozen bits of the current register subtree's real u range
     PCUB_HD void put(int u) {
-        if (store && (w & gm) == j) A->info[(long long)w * A->B + cw] = (uint8_t)u;
+        if (store && (w & gm) == j) info[(long long)w * B + cw] = (uint8_t)u;
         ++w;
     }
+    PCUB_HD bool frozen(int ub) const { return (fm >> ub) & 1u; }
 };
 
 // Exchange of a whole q-vector with lane ^ MASK.
@@ -158,7 +199,8 @@ PCUB_HD QV<Q> q_shfl(const QV<Q>& v) {
 }
 
 // A real node of M <= G positions, position (lane & (M-1)) in each lane; leaf u
-// indices UB .. UB+M-1.  Returns this lane's symbol of the node's re-encoding.
+// indices UB .. UB+M-1 of the register subtree.  Returns this lane's symbol of
+// the node's re-encoding.
 template <int Q, int M>
 struct QXSub {
     static PCUB_HD int run(const QV<Q>& v, int ub, QInfo& qi, int lane) {
@@ -173,12 +215,12 @@ struct QXSub {
         int ym, yp;
         if constexpr (M == 2) {
             ym = 0;
-            if (!qi.A->frozen[ub]) {
+            if (!qi.frozen(ub)) {
                 ym = q_leaf<Q>(q_minus<Q>(a, b));
                 qi.put(ym);
             }
             yp = 0;
-            if (!qi.A->frozen[ub + 1]) {
+            if (!qi.frozen(ub + 1)) {
                 yp = q_leaf<Q>(q_plus<Q>(a, b, ym));
                 qi.put(yp);
             }
@@ -191,7 +233,7 @@ struct QXSub {
 };
 
 // Register-resident node of L virtual positions (half-split); virtual leaves
-// VB .. VB+L-1, i.e. real u indices VB*G .. (VB+L)*G - 1.
+// VB .. VB+L-1 of the subtree, i.e. its real u indices VB*G .. (VB+L)*G - 1.
 template <int Q, int L, int G>
 struct QSub {
     static PCUB_HD void run(const QV<Q>* v, uint8_t* y, int vb, QInfo& qi, int lane) {
@@ -199,7 +241,7 @@ struct QSub {
             y[0] = (uint8_t)QXSub<Q, G>::run(v[0], vb * G, qi, lane);
         } else if constexpr (L == 1) {
             int u = 0;
-            if (!qi.A->frozen[vb]) {
+            if (!qi.frozen(vb)) {
                 u = q_leaf<Q>(v[0]);
                 qi.put(u);
             }
@@ -224,10 +266,10 @@ struct QSub {
 };
 
 template <int Q>
-PCUB_HD QV<Q> q_load(const double* base, long long pos, long long stride) {
+PCUB_HD QV<Q> q_load(const double* base, long long off) {
     QV<Q> v;
 #pragma unroll
-    for (int x = 0; x < Q; ++x) v.p[x] = base[(pos * Q + x) * stride];
+    for (int x = 0; x < Q; ++x) v.p[x] = base[off + x];
     return v;
 }
 
@@ -253,131 +295,208 @@ PCUB_HD void q_store2(double2* base, long long pos, long long stride, const QV<Q
         st2(base + (pos * QP + h) * stride, double2{v.p[2 * h], (2 * h + 1 < Q) ? v.p[2 * h + 1] : 0.0});
 }
 
-// Value at position p of the depth-a node on the current chain: the raw root for
-// a == 0 (half-split position p = natural row bitrev_n(p)), else stage level a.
-struct QLev {
-    const double* in;   // root: row i, symbol x at in[(i * B) * Q + x]
+// One pass of a chain: source depth a (the raw root when a == 0), levels
+// a+1 .. a+F evaluated column by column.  Column c (C = La >> F columns) holds
+// level a+e at positions c + m*C, m < 2^(F-e).
+struct QPass {
+    const double* in;     // root: half-split position p of lane j is row rowbase + bitrev_{nv}(p)
     long long B;
-    int n;
-    const double2* scr;
+    int nv;               // log2 of the virtual (per-lane) length
+    const double2* src;   // stored source level (a > 0)
+    double2* lev[4];      // destinations: levels a+1 .. a+F (stored ones)
     long long ns;
-    int N;
-    template <int Q>
-    PCUB_HD QV<Q> get(int a, int p) const {
-        if (a == 0) return q_load<Q>(in, (long long)bitrev((uint32_t)p, n) * B, 1);
-        return q_load2<Q>(scr, (long long)N - 2 * (N >> a) + p, ns);
+    const uint32_t* Y;    // re-encoded symbols (plus transform decisions)
+    int ystart;           // first Y position of the minus child at depth a+1
+};
+
+template <int Q, bool ROOT>
+PCUB_HD QV<Q> q_src(const QPass& P, int pos) {
+    if constexpr (ROOT) return q_load<Q>(P.in, (long long)bitrev((uint32_t)pos, P.nv) * P.B * Q);
+    else return q_load2<Q>(P.src, pos, P.ns);
+}
+
+// Value of level a+E at index M of column c (position c + M*C), depth-first; every
+// level below a+F, and a+F itself unless FINAL, is stored on the way.
+template <int Q, int F, int E, int M, bool GOP, bool ROOT, bool FINAL>
+struct QCol {
+    static PCUB_HD QV<Q> run(const QPass& P, int c, int C) {
+        QV<Q> v;
+        if constexpr (E == 1) {
+            const QV<Q> x0 = q_src<Q, ROOT>(P, c + M * C);
+            const QV<Q> x1 = q_src<Q, ROOT>(P, c + (M + (1 << (F - 1))) * C);
+            if constexpr (GOP) v = q_plus<Q>(x0, x1, q_sym(P.Y, P.ns, P.ystart + c + M * C));
+            else v = q_minus<Q>(x0, x1);
+        } else {
+            const QV<Q> l = QCol<Q, F, E - 1, M, GOP, ROOT, FINAL>::run(P, c, C);
+            const QV<Q> r = QCol<Q, F, E - 1, M + (1 << (F - E)), GOP, ROOT, FINAL>::run(P, c, C);
+            v = q_minus<Q>(l, r);
+        }
+        if constexpr (E < F || !FINAL) q_store2<Q>(P.lev[E - 1], c + M * C, P.ns, v);
+        return v;
     }
 };
 
+// Non-final pass over all La >> F columns (U columns per iteration: loads of the
+// next column in flight while the current one computes).
+template <int Q, int F, bool GOP, bool ROOT, int U = 1>
+PCUB_HD void q_pass(const QPass& P, int La) {
+    const int C = La >> F;
+    if constexpr (U == 1) {
+#pragma unroll 1
+        for (int c = 0; c < C; ++c) QCol<Q, F, F, 0, GOP, ROOT, false>::run(P, c, C);
+    } else {
+        int c = 0;
+#pragma unroll 1
+        for (; c + U <= C; c += U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) QCol<Q, F, F, 0, GOP, ROOT, false>::run(P, c + u, C);
+        }
+#pragma unroll 1
+        for (; c < C; ++c) QCol<Q, F, F, 0, GOP, ROOT, false>::run(P, c, C);
+    }
+}
+
+// Final pass: level D (S values) into registers.
+template <int Q, int S, int F, bool GOP, bool ROOT>
+PCUB_HD void q_final(const QPass& P, QV<Q>* v) {
+#pragma unroll
+    for (int c = 0; c < S; ++c) v[c] = QCol<Q, F, F, 0, GOP, ROOT, true>::run(P, c, S);
+}
+
+template <int Q, int F, int U>
+PCUB_HD void q_pass_dispatch(const QPass& P, int La, bool gop, bool root) {
+    if (root) {
+        if (gop) q_pass<Q, F, true, true, U>(P, La);
+        else q_pass<Q, F, false, true, U>(P, La);
+    } else {
+        if (gop) q_pass<Q, F, true, false, U>(P, La);
+        else q_pass<Q, F, false, false, U>(P, La);
+    }
+}
+
+template <int Q, int S, int F>
+PCUB_HD void q_final_dispatch(const QPass& P, QV<Q>* v, bool gop, bool root) {
+    if (root) {
+        if (gop) q_final<Q, S, F, true, true>(P, v);
+        else q_final<Q, S, F, false, true>(P, v);
+    } else {
+        if (gop) q_final<Q, S, F, true, false>(P, v);
+        else q_final<Q, S, F, false, false>(P, v);
+    }
+}
+
 // S = register positions per lane (a power of two), G lanes per codeword
-// (lane j of them, `lane` = wave lane id); requires N >= 2*S*G.  Below, n and N
-// are the virtual (per-lane) tree: n = log2(N_real / G).
-template <int Q, int S, int G = 1>
+// (lane j of them, `lane` = wave lane id); requires N >= 2*S*G and S*G <= 32.
+template <int Q, int S, int G = 1, int U = 1>
 PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store, int j = 0, int lane = 0) {
     constexpr int s = (S == 1) ? 0 : (S == 2) ? 1 : (S == 4) ? 2 : (S == 8) ? 3 : 4;
     constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : 2;
+    constexpr int SU = S * G;  // real u positions per register subtree
+    constexpr int QP = (Q + 1) / 2;
     static_assert(G == 1 || G == 2 || G == 4, "lanes per codeword");
-    const int n = A.n - g;
-    const int N = 1 << n;
+    static_assert(SU <= 32, "a register subtree's frozen bits fit one word");
+    const int nv = A.n - g;
+    const int Nv = 1 << nv;
     const long long ns = A.nslots;
-    const int D = n - s;  // depth of the register nodes
+    const int D = nv - s;  // depth of the register nodes
     double2* scr = A.scratch + slot;
     uint32_t* Y = A.ysym + slot;
-    // root rows of lane j: real position j + G*t is row bitrev_n(j) + bitrev_{n-g}(t)
-    QLev lv{A.xy + (cw + (long long)bitrev((uint32_t)j, A.n) * A.B) * Q, A.B, n, scr, ns, N};
-    QInfo qi{&A, cw, store, 0, j, G - 1};
+    // root rows of lane j: real position j + G*t is row bitrev_n(j) + bitrev_{nv}(t)
+    const double* in = A.xy + (cw + (long long)bitrev((uint32_t)j, A.n) * A.B) * Q;
+    QInfo qi{A.info, A.B, cw, store, 0, j, G - 1, 0u};
     for (int k = 0; k < (1 << D); ++k) {
+        in = launder(in);
+        scr = launder(scr);
+        Y = launder(Y);
         const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
         const int e0 = A.ef[k];  // first all-frozen depth on this chain (D + 1: none)
         const int stop = e0 <= D ? e0 - 1 : D;  // deepest level to evaluate
         int a = d0 - 1;
         bool gop = (k != 0);
-        // stored levels a+1 .. min(stop, D-1), two per pass
-        while (a < (stop < D ? stop : D - 1)) {
-            const int last = stop < D ? stop : D - 1;
-            const int F = (last - a) >= 2 ? 2 : 1;
-            const int La = N >> a;
-            const int ystart = (k >> (D - a)) << (n - a);  // minus child's first Y position
-            if (F == 2) {
-                const int C = La >> 2;
-                for (int p = 0; p < C; ++p) {
-                    QV<Q> l1[2];
+        QPass P;
+        P.in = in;
+        P.B = A.B;
+        P.nv = nv;
+        P.ns = ns;
+        P.Y = Y;
+        // passes of up to three levels, greedily from the top; the last one (when the
+        // chain reaches depth D) lands in registers
+        while (true) {
+            const int last = stop;  // deepest level of this chain
+            const int T = last - a;
+            if (T <= 0) break;
+            const bool fin = (last == D) && T <= 3;
+            const int F = T >= 3 ? 3 : T;
+            P.src = a > 0 ? scr + (long long)(Nv - 2 * (Nv >> a)) * QP * ns : nullptr;
+            P.ystart = (k >> (D - a)) << (nv - a);
 #pragma unroll
-                    for (int m = 0; m < 2; ++m) {
-                        const QV<Q> x0 = lv.template get<Q>(a, p + m * C), x1 = lv.template get<Q>(a, p + (m + 2) * C);
-                        l1[m] = gop ? q_plus<Q>(x0, x1, q_sym(Y, ns, ystart + p + m * C)) : q_minus<Q>(x0, x1);
-                        q_store2<Q>(scr, (long long)N - 2 * (N >> (a + 1)) + p + m * C, ns, l1[m]);
-                    }
-                    q_store2<Q>(scr, (long long)N - 2 * (N >> (a + 2)) + p, ns, q_minus<Q>(l1[0], l1[1]));
-                }
-            } else {
-                const int C = La >> 1;
-                for (int p = 0; p < C; ++p) {
-                    const QV<Q> x0 = lv.template get<Q>(a, p), x1 = lv.template get<Q>(a, p + C);
-                    const QV<Q> o = gop ? q_plus<Q>(x0, x1, q_sym(Y, ns, ystart + p)) : q_minus<Q>(x0, x1);
-                    q_store2<Q>(scr, (long long)N - 2 * (N >> (a + 1)) + p, ns, o);
-                }
-            }
+            for (int e = 1; e <= 3; ++e)
+                P.lev[e - 1] = (a + e < D) ? scr + (long long)(Nv - 2 * (Nv >> (a + e))) * QP * ns : nullptr;
+            if (fin) break;
+            const int La = Nv >> a;
+            if (F == 3) q_pass_dispatch<Q, 3, U>(P, La, gop, a == 0);
+            else if (F == 2) q_pass_dispatch<Q, 2, U>(P, La, gop, a == 0);
+            else q_pass_dispatch<Q, 1, U>(P, La, gop, a == 0);
             a += F;
             gop = false;
         }
         uint8_t y[S];
         if (stop == D) {
-            // level D into registers, then the register subtree
-            const int ystart = (k >> (D - a)) << (n - a);
             QV<Q> v[S];
-#pragma unroll
-            for (int p = 0; p < S; ++p) {
-                const QV<Q> x0 = lv.template get<Q>(a, p), x1 = lv.template get<Q>(a, p + S);
-                v[p] = gop ? q_plus<Q>(x0, x1, q_sym(Y, ns, ystart + p)) : q_minus<Q>(x0, x1);
-            }
-            QSub<Q, S, G>::run(v, y, k * S, qi, lane);
+            const int F = D - a;
+            if (F == 3) q_final_dispatch<Q, S, 3>(P, v, gop, a == 0);
+            else if (F == 2) q_final_dispatch<Q, S, 2>(P, v, gop, a == 0);
+            else q_final_dispatch<Q, S, 1>(P, v, gop, a == 0);
+            const int us = k * SU;
+            qi.fm = (A.fwords[us >> 5] >> (us & 31));
+            QSub<Q, S, G>::run(v, y, 0, qi, lane);
         } else {
 #pragma unroll
-            for (int j = 0; j < S; ++j) y[j] = 0;  // rate-0: symbols 0, re-encoding 0
+            for (int t = 0; t < S; ++t) y[t] = 0;  // rate-0: symbols 0, re-encoding 0
         }
         // the subtree's symbols into its words (S < 4: a part of one word)
         if constexpr (S >= 4) {
 #pragma unroll
             for (int w = 0; w < S / 4; ++w)
-                Y[(long long)(k * S / 4 + w) * ns] = (uint32_t)y[4 * w] | ((uint32_t)y[4 * w + 1] << 8) |
-                                                     ((uint32_t)y[4 * w + 2] << 16) | ((uint32_t)y[4 * w + 3] << 24);
+                stu(Y + (long long)(k * S / 4 + w) * ns, (uint32_t)y[4 * w] | ((uint32_t)y[4 * w + 1] << 8) |
+                                                             ((uint32_t)y[4 * w + 2] << 16) | ((uint32_t)y[4 * w + 3] << 24));
         } else {
             uint32_t* yw = Y + (long long)((k * S) >> 2) * ns;
             const int sh = ((k * S) & 3) * 8;
             uint32_t ws = 0;
 #pragma unroll
-            for (int j = 0; j < S; ++j) ws |= (uint32_t)y[j] << (8 * j);
-            *yw = (sh == 0 ? 0u : (*yw & ((1u << sh) - 1u))) | (ws << sh);
+            for (int t = 0; t < S; ++t) ws |= (uint32_t)y[t] << (8 * t);
+            stu(yw, (sh == 0 ? 0u : (ldu(yw) & ((1u << sh) - 1u))) | (ws << sh));
         }
         // combine completed plus children: [(ym+yp)%q | (q-yp)%q]
         for (int d = D; d >= 1 && ((k >> (D - d)) & 1); --d) {
-            const int Lc = N >> d;
+            const int Lc = Nv >> d;
             const long long st = (long long)(k >> (D - d + 1)) * 2 * Lc;
             if (Lc >= 4) {
                 for (int w = 0; w < Lc / 4; ++w) {
                     uint32_t* pm = Y + (st / 4 + w) * ns;
                     uint32_t* pp = Y + (st / 4 + Lc / 4 + w) * ns;
-                    uint32_t m = *pm, p = *pp;
+                    uint32_t m = ldu(pm), p = ldu(pp);
                     q_combine_words<Q>(m, p);
-                    *pm = m;
-                    *pp = p;
+                    stu(pm, m);
+                    stu(pp, p);
                 }
             } else {  // Lc = 1, 2: the parent is 2 or 4 bytes of one word
                 uint32_t* pw = Y + (st >> 2) * ns;
                 const int sh = (int)(st & 3) * 8;
                 const uint32_t lm = (Lc == 1) ? 0xffu : 0xffffu;
-                uint32_t m = (*pw >> sh) & lm, p = (*pw >> (sh + 8 * Lc)) & lm;
+                const uint32_t w0 = ldu(pw);
+                uint32_t m = (w0 >> sh) & lm, p = (w0 >> (sh + 8 * Lc)) & lm;
                 q_combine_words<Q>(m, p);
-                *pw = (*pw & ~(((lm << (8 * Lc)) | lm) << sh)) | (((p << (8 * Lc)) | m) << sh);
+                stu(pw, (w0 & ~(((lm << (8 * Lc)) | lm) << sh)) | (((p << (8 * Lc)) | m) << sh));
             }
         }
     }
     // x_hat[i] is the root's half-split position bitrev(i): lane j holds the rows
-    // bitrev_n(j) + bitrev_{n-g}(t), t = its local position
+    // bitrev_n(j) + bitrev_{nv}(t), t = its local position
     if (A.xhat && store) {
         uint8_t* xo = A.xhat + cw + (long long)bitrev((uint32_t)j, A.n) * A.B;
-        for (int t = 0; t < N; ++t) xo[(long long)bitrev((uint32_t)t, n) * A.B] = (uint8_t)q_sym(Y, ns, t);
+        for (int t = 0; t < Nv; ++t) xo[(long long)bitrev((uint32_t)t, nv) * A.B] = (uint8_t)q_sym(Y, ns, t);
     }
 }
 

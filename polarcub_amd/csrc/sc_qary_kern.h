@@ -1,0 +1,86 @@
+// sc_qary_kern.h -- the q-ary SC decode kernel template and its instantiation table.
+//
+// Instantiated per alphabet size in sc_qary_q*.hip (the q-ary schedules are large
+// templates: one translation unit per q keeps the parallel build short); sc_qary.hip
+// owns the launch code.  Geometries: S register positions per lane x G lanes per
+// codeword, only those q_geom() can pick (S = 8 for q <= 4 else 4, G = 4, both
+// reduced for short codes).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "sc_qary_body.h"
+
+namespace pcub {
+
+constexpr int kQaryBlock = 256;
+
+// waves per SIMD the register allocation must allow: the S*q doubles of the register
+// level (and q >= 6 vectors in the transforms) need two waves' worth of registers at
+// 32; up to 16 the kernel runs at four (the fastest q = 4 geometry, S = 4, G = 4:
+// 73.4M cw/s at 4 waves vs 71.0M at 3, profiles/r2/qary_*)
+constexpr int qary_waves(int q, int S) { return (q * S >= 32 || q >= 6) ? 2 : (q * S <= 16 ? 4 : 3); }
+
+template <int Q, int S, int G, int W = qary_waves(Q, S), int U = 1>
+__global__ __launch_bounds__(kQaryBlock, W) void k_sc_qary(QArgs A) {
+    constexpr int CWB = kQaryBlock / G;  // codewords per tile
+    const long long slot = (long long)blockIdx.x * kQaryBlock + threadIdx.x;
+    const int j = threadIdx.x & (G - 1);
+    const int lane = threadIdx.x & 63;
+    const long long ntiles = (A.B + CWB - 1) / CWB;
+    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const long long cw = t * CWB + threadIdx.x / G;
+        const bool valid = cw < A.B;
+        decode_qary_cw<Q, S, G, U>(A, valid ? cw : A.B - 1, slot, valid, j, lane);
+    }
+}
+
+typedef void (*QKern)(QArgs);
+
+// the kernel for (q, S, G), or nullptr
+QKern qary_kernel_q2(int S, int G);
+QKern qary_kernel_q3(int S, int G);
+QKern qary_kernel_q4(int S, int G);
+QKern qary_kernel_q56(int q, int S, int G);
+QKern qary_kernel_q78(int q, int S, int G);
+
+inline QKern qary_kernel(int q, int S, int G) {
+    switch (q) {
+        case 2: return qary_kernel_q2(S, G);
+        case 3: return qary_kernel_q3(S, G);
+        case 4: return qary_kernel_q4(S, G);
+        case 5:
+        case 6: return qary_kernel_q56(q, S, G);
+        case 7:
+        case 8: return qary_kernel_q78(q, S, G);
+        default: return nullptr;
+    }
+}
+
+// geometries q_geom() can produce for a large S0 (8 or 4): S in {S0, S0/2} with
+// G = 4, 2, 1, and smaller S with G = 1 (short codes)
+template <int Q, int S0>
+QKern qary_kernel_geom(int S, int G) {
+    constexpr int S1 = S0 / 2;
+    if (S == S0 || S == S1) {
+        if (S == S0) {
+            if (G == 4) return k_sc_qary<Q, S0, 4>;
+            if (G == 2) return k_sc_qary<Q, S0, 2>;
+            if (G == 1) return k_sc_qary<Q, S0, 1>;
+        } else {
+            if (G == 4) return k_sc_qary<Q, S1, 4>;
+            if (G == 2) return k_sc_qary<Q, S1, 2>;
+            if (G == 1) return k_sc_qary<Q, S1, 1>;
+        }
+        return nullptr;
+    }
+    if (G != 1) return nullptr;
+    if constexpr (S1 > 2) {
+        if (S == S1 / 2) return k_sc_qary<Q, S1 / 2, 1>;
+    }
+    if constexpr (S1 > 1) {
+        if (S == 1) return k_sc_qary<Q, 1, 1>;
+    }
+    return nullptr;
+}
+
+}  // namespace pcub

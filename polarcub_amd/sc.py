@@ -134,6 +134,15 @@ def set_qary_lanes(g):
     return old
 
 
+def set_qary_regs(s):
+    """Cap on the q-ary decode kernel's register positions per lane (0 = default, 2, 4 or
+    8).  Returns the previous setting."""
+    old = int(_lib.lib().pcub_sc_set_qary_regs(int(s)))
+    if old < 0:
+        raise ValueError("q-ary register positions must be 0, 2, 4 or 8")
+    return old
+
+
 def variants():
     """[(S, G, W)] per decode kernel variant: register-subtree values per lane,
     lanes per codeword, minimum waves per SIMD."""

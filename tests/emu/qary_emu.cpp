@@ -8,6 +8,11 @@
 
 using namespace pcub;
 
+template <int Q, int S>
+static void run_s(const QArgs& A, long long B) {
+    for (long long b = 0; b < B; ++b) decode_qary_cw<Q, S>(A, b, b % A.nslots, true);
+}
+
 template <int Q>
 static int run(const double* xy, long long B, int n, const uint8_t* frozen, uint8_t* info, uint8_t* xhat, int S) {
     const int N = 1 << n;
@@ -25,20 +30,19 @@ static int run(const double* xy, long long B, int n, const uint8_t* frozen, uint
     A.xy = xy;
     A.B = B;
     A.n = n;
-    A.frozen = frozen;
+    A.fwords = words.data();
     A.ef = ef.data();
     A.info = info;
     A.xhat = xhat;
     A.scratch = scr.data();
     A.ysym = ys.data();
     A.nslots = ns;
-    for (long long b = 0; b < B; ++b) {
-        switch (S) {
-            case 1: decode_qary_cw<Q, 1>(A, b, b % ns, true); break;
-            case 2: decode_qary_cw<Q, 2>(A, b, b % ns, true); break;
-            case 4: decode_qary_cw<Q, 4>(A, b, b % ns, true); break;
-            default: decode_qary_cw<Q, 8>(A, b, b % ns, true); break;
-        }
+    switch (S) {
+        case 1: run_s<Q, 1>(A, B); break;
+        case 2: run_s<Q, 2>(A, B); break;
+        case 4: run_s<Q, 4>(A, B); break;
+        case 8: run_s<Q, 8>(A, B); break;
+        default: run_s<Q, 16>(A, B); break;
     }
     return 0;
 }
@@ -55,4 +59,20 @@ extern "C" int emu_decode_qary(const double* xy, long long B, int n, int q, cons
         case 8: return run<8>(xy, B, n, frozen, info, xhat, S);
         default: return -1;
     }
+}
+
+// q_div (shared reciprocal + Markstein correction, guarded) against plain IEEE
+// division: `count` quadruples (p0..p3, t) from the caller, returns the mismatches.
+extern "C" long long emu_qdiv_check(const double* p, const double* t, long long count) {
+    long long bad = 0;
+    for (long long i = 0; i < count; ++i) {
+        QV<4> v;
+        for (int x = 0; x < 4; ++x) v.p[x] = p[4 * i + x];
+        q_div<4>(v, t[i]);
+        for (int x = 0; x < 4; ++x) {
+            const double want = p[4 * i + x] / t[i];
+            if (__builtin_memcmp(&want, &v.p[x], sizeof(double)) != 0) ++bad;
+        }
+    }
+    return bad;
 }

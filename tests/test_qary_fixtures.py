@@ -107,7 +107,7 @@ def test_qary_encode_decode_simulation_prints_reference_line(run):
     g = load_golden("qary_harness")
     r = g["meta"]["runs"][run]
     q, N = r["q"], 1 << r["n"]
-    frozen = set(int(i) for i in np.nonzero(g[r["name"] + "_frozen"])[0])
+    frozen = set(int(i) for i in np.nonzero(load_golden("construct_qary")[r["frozen_key"]])[0])
     make_x, channel, make_xy = _qary_closures(q, N, r["p"])
     random.seed(r["global_seed"])
     buf = io.StringIO()

@@ -91,7 +91,8 @@ class Awgn:
 
     def __init__(self, a, device, rank):
         self.a = a
-        n, N = a.n, 1 << a.n
+        n = a.n if a.n is not None else 10
+        N = 1 << n
         K = int(round(N * a.rate))
         self.n, self.N, self.K, self.B = n, N, K, a.batch
         self.sigma2 = construction.awgn_sigma2(a.ebn0, K / N)
@@ -178,29 +179,56 @@ class Awgn:
                           "on %s (%.1f CPU-s)" % (ncw, reps, code.N, cdesc, dt * cores)}
 
 
+def _genie_file_scores(path):
+    """Per-index genie counts (TV + Pe summed over the trials) of a frozen-set file in the
+    format of BinaryPolarEncoderDecoder.py:471-489 ('*** i count' lines), and the frozen set
+    (index lines)."""
+    scores, frozen = {}, set()
+    with open(path) as f:
+        for line in f:
+            if line.startswith("***"):
+                _, i, c = line.split()
+                scores[int(i)] = float(c)
+            elif not line.startswith("*") and line.strip():
+                frozen.add(int(line))
+    return scores, frozen
+
+
 class Deletion:
-    """Deletion channel, main_deletion.py defaults (configs[4]): n=8, n0=2, pd=0.1, xi=0.1.
-    Frozen set: the N/4 most reliable indices by the reference's genie ranking (fixture)."""
+    """Deletion channel, configs[4] = main_deletion.py's configuration: n=8, n0=n//3=2,
+    pd=0.1, xi=0.1, no guard-band ones; the frozen set of its default construction (genie,
+    -g 8000, -pe 0.1: K=3, tests/golden/frozen_deletion_n8_g8000.txt written by this
+    framework's main_deletion counterpart), or with --del-k K the K indices of smallest genie
+    TV+Pe (a heavier decode).  Other n: n0 = n//3 unless --n0, frozen set = the N/4 most
+    reliable indices of a Bhattacharyya ranking (stand-in; no genie fixture at that size)."""
     kernel = "k_sc_del"
 
     def __init__(self, a, device, rank):
         self.a = a
-        self.n, self.n0, self.pd, self.xi = a.n if a.n != 10 else 8, a.n0, a.pd, a.xi
+        self.n = a.n if a.n is not None else 8
+        self.n0 = a.n0 if a.n0 is not None else self.n // 3
+        self.pd, self.xi, self.ones = a.pd, a.xi, a.ones
         self.N = 1 << self.n
         self.B = a.batch
-        g = np.load(os.path.join(ROOT, "tests", "golden", "deletion_n8.npz"), allow_pickle=False)
-        if self.n == 8:
-            score = g["genie_score"]
-            order = sorted(range(self.N), key=lambda i: (score[i], i))
-            frozen = set(order[self.N // 4:])
+        if self.n == 8 and self.n0 == 2 and abs(self.pd - 0.1) < 1e-12 and abs(self.xi - 0.1) < 1e-12:
+            scores, frozen = _genie_file_scores(os.path.join(ROOT, "tests", "golden", "frozen_deletion_n8_g8000.txt"))
+            if a.del_k:
+                order = sorted(range(self.N), key=lambda i: (scores[i], i))
+                frozen = set(order[a.del_k:])
+                self.construction = "genie (8000 trials) ranking, K=%d" % a.del_k
+            else:
+                self.construction = "main_deletion.py default construction: genie 8000 trials, Pe bound 0.1"
         else:
-            frozen = set(np.nonzero(construction.bhattacharyya_frozen(self.n, self.N // 4, 0.5))[0].tolist())
+            K = a.del_k or self.N // 4
+            frozen = set(np.nonzero(construction.bhattacharyya_frozen(self.n, K, 0.5))[0].tolist())
+            self.construction = "Bhattacharyya ranking stand-in, K=%d" % K
         self.code = sc.CodeSpec.from_frozen_set(self.N, frozen, 200, device=device)
         self.K = self.code.K
-        self.dec = sc.DeletionDecoder(self.code, self.n0, self.pd)
+        self.dec = sc.DeletionDecoder(self.code, self.n0, self.pd, self.ones)
         gen = torch.Generator(device=device)
         gen.manual_seed(mc.shard_seed(a.seed, rank))
-        self.rx, self.rx_len, self.info_tx = mc.deletion_batch(self.code, self.B, self.n0, self.xi, self.pd, gen)
+        self.rx, self.rx_len, self.info_tx = mc.deletion_batch(self.code, self.B, self.n0, self.xi, self.pd, gen,
+                                                               ones=self.ones)
         self.outs = None
 
     def step(self):
@@ -213,7 +241,7 @@ class Deletion:
         return float(self.rx_len.float().mean().item()) + 4 + self.N // 8 + self.K // 8
 
     def tag(self):
-        return "del_n%d_n0%d" % (self.n, self.n0)
+        return "del_n%d_n0%d%s" % (self.n, self.n0, "_k%d" % self.K if self.K != 3 else "")
 
     def describe(self, world):
         return dict(
@@ -222,9 +250,11 @@ class Deletion:
             dtype="f64",
             data="synthetic: uniform info bits, GPU polar encoder, guard bands (xi=%.2f), deletions drawn on device"
                  % self.xi,
-            config={"workload": "deletion SC decode N=%d n0=%d K=%d pd=%.2f (BASELINE configs[4])"
-                                % (self.N, self.n0, self.K, self.pd),
-                    "N": self.N, "K": self.K, "n0": self.n0, "pd": self.pd, "xi": self.xi, "batch_per_gpu": self.B,
+            config={"workload": "deletion SC decode N=%d n0=%d K=%d pd=%.2f ones=%d%s"
+                                % (self.N, self.n0, self.K, self.pd, self.ones,
+                                   " (BASELINE configs[4])" if self.n == 8 else ""),
+                    "N": self.N, "K": self.K, "n0": self.n0, "pd": self.pd, "xi": self.xi, "ones": self.ones,
+                    "frozen_set": self.construction, "batch_per_gpu": self.B,
                     "received_len_mean": float(self.rx_len.float().mean().item()),
                     "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
 
@@ -270,7 +300,7 @@ class Qary:
 
     def __init__(self, a, device, rank):
         self.a = a
-        self.q, self.n = a.q, (a.n if a.n != 10 else 8)
+        self.q, self.n = a.q, (a.n if a.n is not None else 8)
         self.N = 1 << self.n
         self.K = self.N // 2
         self.B = a.batch
@@ -429,10 +459,12 @@ def build_parser():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="awgn")
-    ap.add_argument("--n", type=int, default=10, help="log2 code length (awgn; deletion/qary default 8)")
+    ap.add_argument("--n", type=int, default=None, help="log2 code length (default: awgn 10, deletion / qary 8)")
     ap.add_argument("--rate", type=float, default=0.5)
     ap.add_argument("--ebn0", type=float, default=2.0)
-    ap.add_argument("--n0", type=int, default=2, help="deletion: log2 inputs per trellis")
+    ap.add_argument("--n0", type=int, default=None, help="deletion: log2 inputs per trellis (default n // 3)")
+    ap.add_argument("--ones", type=int, default=0, help="deletion: guard-band ones (numberOfOnesToAddAtBothEndsOfGuardbands)")
+    ap.add_argument("--del-k", type=int, default=0, help="deletion: information bits (0 = the configuration's frozen set)")
     ap.add_argument("--pd", type=float, default=0.1, help="deletion probability")
     ap.add_argument("--xi", type=float, default=0.1, help="guard-band parameter")
     ap.add_argument("--q", type=int, default=4)

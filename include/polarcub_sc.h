@@ -20,7 +20,8 @@
  * Conventions
  *   - All data pointers are DEVICE pointers (hipMalloc'd or torch CUDA tensors).
  *   - `stream` is a hipStream_t passed as void* (NULL = default stream); every
- *     call is stream-ordered and asynchronous; no call synchronises or allocates.
+ *     call is stream-ordered and asynchronous; no call synchronises, and none
+ *     allocates except pcub_polar_encode_bin for log2N > 14 (stream-ordered scratch).
  *   - Bit vectors are "word-major, codeword-minor": word w of codeword b is at
  *     words[w * B + b] (32 bits per word, bit t = element 32w+t).  This is the
  *     coalesced layout for one-codeword-per-lane kernels.
@@ -89,20 +90,23 @@ int pcub_polar_encode_qary(const uint8_t* info, int64_t B, int32_t log2N, int32_
 int pcub_polar_encode_bin(const uint32_t* info_words, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
                           const uint32_t* frozen_val, int32_t K, uint32_t* x_words, void* stream);
 
-/* SC decode over the deletion channel (uniform input, no guard-band ones): replaces
+/* SC decode over the deletion channel (uniform input): replaces
  * BinaryPolarEncoderDecoder.decode (BinaryPolarEncoderDecoder.py:71-99) over the
  * CollectionOfBinaryTrellises that buildCollectionOfBinaryTrellises_uniformInput_deletion
  * (VectorDistributions/CollectionOfBinaryTrellises.py:106-129, BinaryTrellis.py:309-438,
  * Guardbands.py:47-93) builds from each received word.
  *   rx          [B][stride] u8 received symbols (0/1), rx_len[b] <= stride of them valid
- *   n, n0       code length 2^n, 2^n0 inputs per trellis; supported: 1 <= n0 <= 3,
- *               1 <= n - n0 <= 6 (pcub_sc_deletion_supported)
+ *   n, n0       code length 2^n, 2^n0 inputs per trellis; supported (decode):
+ *               1 <= n0 <= 4, 1 <= n - n0 <= 8; leaf export: n - n0 <= 6 and ones = 0
+ *               (pcub_sc_deletion_supported / pcub_sc_leaf_deletion_supported)
+ *   ones        numberOfOnesToAddAtBothEndsOfGuardbands, 0 <= ones <= 3
  *   pd          deletion probability the trellises are built with
  *   frozen_mask / frozen_val / K / info_words / xhat_words as pcub_sc_decode_bin. */
-int pcub_sc_deletion_supported(int32_t n, int32_t n0);
+int pcub_sc_deletion_supported(int32_t n, int32_t n0, int32_t ones);
+int pcub_sc_leaf_deletion_supported(int32_t n, int32_t n0, int32_t ones);
 int pcub_sc_decode_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n, int32_t n0,
-                            double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K,
-                            uint32_t* info_words, uint32_t* xhat_words, void* stream);
+                            int32_t ones, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
+                            int32_t K, uint32_t* info_words, uint32_t* xhat_words, void* stream);
 
 /* Leaf export (LLR check, genie construction).  Decodes like pcub_sc_decode_bin /
  * pcub_sc_decode_deletion (identical decisions) and also writes, for every u index i,
@@ -119,7 +123,7 @@ int pcub_sc_leaf_bin(const double* xy, int64_t B, int32_t log2N, const uint32_t*
                      const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words, double* leaf,
                      void* workspace, size_t workspace_bytes, void* stream);
 int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n, int32_t n0,
-                          double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
+                          int32_t ones, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
                           const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
                           double* leaf, void* stream);
 /* compact leaves -> the reference's marginals (calcMarginalizedProbabilities,

@@ -15,6 +15,7 @@ _i32 = ctypes.c_int32
 _lib = None
 
 EINVAL = -1
+ABI_VERSION = 2  # include/polarcub_sc.h (2: guard-band ones in the deletion entry points)
 
 
 class HipError(RuntimeError):
@@ -68,9 +69,11 @@ def lib():
     L.pcub_transpose_pairs.restype = ctypes.c_int
     L.pcub_transpose_pairs.argtypes = [_c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p]
     L.pcub_sc_deletion_supported.restype = ctypes.c_int
-    L.pcub_sc_deletion_supported.argtypes = [_i32, _i32]
+    L.pcub_sc_deletion_supported.argtypes = [_i32, _i32, _i32]
+    L.pcub_sc_leaf_deletion_supported.restype = ctypes.c_int
+    L.pcub_sc_leaf_deletion_supported.argtypes = [_i32, _i32, _i32]
     L.pcub_sc_decode_deletion.restype = ctypes.c_int
-    L.pcub_sc_decode_deletion.argtypes = [_c_void_p, _c_void_p, _i64, _i32, _i32, _i32, ctypes.c_double, _c_void_p,
+    L.pcub_sc_decode_deletion.argtypes = [_c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, ctypes.c_double, _c_void_p,
                                           _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p]
     L.pcub_sc_leaf_bin_workspace.restype = ctypes.c_size_t
     L.pcub_sc_leaf_bin_workspace.argtypes = [_i64, _i32]
@@ -78,7 +81,7 @@ def lib():
     L.pcub_sc_leaf_bin.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                                    _c_void_p, _c_void_p, ctypes.c_size_t, _c_void_p]
     L.pcub_sc_leaf_deletion.restype = ctypes.c_int
-    L.pcub_sc_leaf_deletion.argtypes = [_c_void_p, _c_void_p, _i64, _i32, _i32, _i32, ctypes.c_double, _c_void_p,
+    L.pcub_sc_leaf_deletion.argtypes = [_c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _i32, ctypes.c_double, _c_void_p,
                                         _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p]
     L.pcub_leaf_marginals.restype = ctypes.c_int
     L.pcub_leaf_marginals.argtypes = [_c_void_p, _i64, _c_void_p, _c_void_p]
@@ -94,7 +97,7 @@ def lib():
     L.pcub_mc_run_bin.restype = ctypes.c_int
     L.pcub_mc_run_bin.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p, _i32, _i64,
                                   _c_void_p, _c_void_p, ctypes.c_size_t, _c_void_p]
-    if L.pcub_abi_version() != 1:
+    if L.pcub_abi_version() != ABI_VERSION:
         raise ImportError("libpolarcub_hip.so ABI mismatch; rebuild with python -m polarcub_amd.build --force")
     _lib = L
     return L
@@ -104,7 +107,7 @@ def lib():
 EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_bin", "pcub_polar_encode_bin",
            "pcub_sc_decode_qary_workspace", "pcub_sc_decode_qary", "pcub_polar_encode_qary",
            "pcub_pack_bits", "pcub_unpack_bits", "pcub_transpose_pairs", "pcub_sc_deletion_supported",
-           "pcub_sc_decode_deletion", "pcub_sc_leaf_bin_workspace", "pcub_sc_leaf_bin", "pcub_sc_leaf_deletion",
+           "pcub_sc_leaf_deletion_supported", "pcub_sc_decode_deletion", "pcub_sc_leaf_bin_workspace", "pcub_sc_leaf_bin", "pcub_sc_leaf_deletion",
            "pcub_leaf_marginals", "pcub_mc_info", "pcub_mc_channel", "pcub_mc_count_errors",
            "pcub_mc_run_bin_workspace", "pcub_mc_run_bin"]
 

@@ -44,16 +44,19 @@ def guard_band_positions(n, n0, xi, ones=0):
     return pos, len(marked), [j for j, v in enumerate(marked) if v == 1]
 
 
-def deletion_words(x_bn, n, n0, xi, pd, generator=None):
-    """x_bn: [B, N] 0/1 codewords (device) -> guard bands added, every symbol deleted
-    independently with probability pd (BinaryTrellis.deletionChannelSimulation's law, drawn
-    with torch's Philox instead of MT19937), survivors packed to the left.
+def deletion_words(x_bn, n, n0, xi, pd, generator=None, ones=0):
+    """x_bn: [B, N] 0/1 codewords (device) -> guard bands added (with `ones` ones at both
+    ends of every guard band), every symbol deleted independently with probability pd
+    (BinaryTrellis.deletionChannelSimulation's law, drawn with torch's Philox instead of
+    MT19937), survivors packed to the left.
     Returns (rx [B, W] uint8, rx_len [B] int32), W = guard-banded length."""
     B, N = x_bn.shape
-    pos, W, ones_pos = guard_band_positions(n, n0, xi)
+    pos, W, ones_pos = guard_band_positions(n, n0, xi, ones)
     dev = x_bn.device
     cw = torch.zeros((B, W), dtype=torch.uint8, device=dev)
     cw[:, torch.tensor(pos, device=dev)] = x_bn.to(torch.uint8)
+    if ones_pos:
+        cw[:, torch.tensor(ones_pos, device=dev)] = 1
     keep = torch.rand((B, W), device=dev, generator=generator) >= pd
     dest = torch.cumsum(keep, dim=1, dtype=torch.int32) - 1
     dest = torch.where(keep, dest, torch.full_like(dest, W))  # deleted symbols go to a trash column

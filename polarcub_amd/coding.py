@@ -50,15 +50,15 @@ def _is_uniform_prior(xvd):
     return p.ndim == 2 and p.shape[1] == 2 and bool(np.all(p[:, 0] == p[:, 1])) and bool(np.all(np.isfinite(p)))
 
 
-def _deletion_kernel_shape(xyvd):
-    """(pd, n, n0) when xyvd is a received-word trellis collection the deletion kernel decodes."""
+def _deletion_kernel_shape(xyvd, leaves=False):
+    """(pd, n, n0, ones) when xyvd is a received-word trellis collection the deletion kernel
+    decodes (leaves=True: the leaf-export kernel, for the genie)."""
     if not deletion.is_deletion_collection(xyvd):
         return None
     word, pd, n, n0, ones = xyvd.deletion_source
-    if ones != 0:
-        return None
     from . import sc
-    return (pd, n, n0) if sc.deletion_supported(n, n0) else None
+    ok = sc.leaf_deletion_supported(n, n0, ones) if leaves else sc.deletion_supported(n, n0, ones)
+    return (pd, n, n0, ones) if ok else None
 
 
 def _check_joint(p):
@@ -132,16 +132,16 @@ class BinaryPolarEncoderDecoder:
         info, xhat = self._decoder.decode(t)
         return xhat.cpu().numpy().astype(np.int64), info.cpu().numpy().astype(np.int64)
 
-    def decode_deletion_batch(self, receivedWords, deletionProb, n0):
+    def decode_deletion_batch(self, receivedWords, deletionProb, n0, ones=0):
         """Received words (0/1 sequences) of the deletion channel -> (encodedVectors int64[B, N],
         information int64[B, k]); the same result as decode() on each word's
-        buildCollectionOfBinaryTrellises_uniformInput_deletion(word, deletionProb, xi, n, n0, 0)."""
+        buildCollectionOfBinaryTrellises_uniformInput_deletion(word, deletionProb, xi, n, n0, ones)."""
         from . import sc
         code = self._code()
-        key = (int(n0), float(deletionProb))
+        key = (int(n0), float(deletionProb), int(ones))
         dec = self._del_decoders.get(key)
         if dec is None:
-            dec = self._del_decoders[key] = sc.DeletionDecoder(code, n0, deletionProb)
+            dec = self._del_decoders[key] = sc.DeletionDecoder(code, n0, deletionProb, ones)
         rx, ln = sc.pad_words(receivedWords, code.device)
         info, xhat = dec.decode(rx, ln)
         return xhat.cpu().numpy().astype(np.int64), info.cpu().numpy().astype(np.int64)
@@ -175,7 +175,8 @@ class BinaryPolarEncoderDecoder:
             return (enc[0], info[0])
         shape = _deletion_kernel_shape(xyVectorDistribution)
         if shape is not None and _is_uniform_prior(xVectorDistribution):
-            enc, info = self.decode_deletion_batch([xyVectorDistribution.deletion_source[0]], shape[0], shape[2])
+            enc, info = self.decode_deletion_batch([xyVectorDistribution.deletion_source[0]], shape[0], shape[2],
+                                                   shape[3])
             return (enc[0], info[0])
         information = np.empty(self.k, np.int64)
         information[:] = -1
@@ -323,7 +324,7 @@ def encodeDecodeSimulation(length, make_xVectorDistribution, make_codeword, simu
         if batch_xy:
             results["bin"] = encDec.decode_batch(np.stack(batch_xy))[1]
         for shape, words in batch_del.items():
-            results[shape] = encDec.decode_deletion_batch(words, shape[0], shape[2])[1]
+            results[shape] = encDec.decode_deletion_batch(words, shape[0], shape[2], shape[3])[1]
         for (t, codeword, received, info_t) in pending:
             if isinstance(info_t, tuple):
                 info_t = results[info_t[0]][info_t[1]]
@@ -399,7 +400,7 @@ def genieEncodeDecodeSimulation(length, make_xVectorDistribution, make_codeword,
             codeword = make_codeword(enc_stats[t][0])
             received = simulateChannel(codeword)
             xyvd = make_xyVectrorDistribution(received)
-            shape = _deletion_kernel_shape(xyvd) if uniform else None
+            shape = _deletion_kernel_shape(xyvd, leaves=True) if uniform else None
             if uniform and _is_memoryless_binary(xyvd) and length >= 2:
                 items.append(("bin", len(bin_rows)))
                 bin_rows.append(_check_joint(xyvd.probs))
@@ -471,10 +472,10 @@ def _device_genie_deletion(length, shape, words, U):
     import torch
 
     from . import sc
-    pd, n, n0 = shape
+    pd, n, n0, ones = shape
     code = sc.CodeSpec(length, np.ones(length, np.uint8), np.zeros(length, np.uint8))
     rx, ln = sc.pad_words(words, code.device)
-    _, _, m = sc.DeletionDecoder(code, n0, pd).decode_leaves(rx, ln, torch.from_numpy(U).to(code.device))
+    _, _, m = sc.DeletionDecoder(code, n0, pd, ones).decode_leaves(rx, ln, torch.from_numpy(U).to(code.device))
     return m.cpu().numpy()
 
 

@@ -127,7 +127,7 @@ int pick_variant(int n) {
 
 }  // namespace
 
-extern "C" int pcub_abi_version(void) { return 1; }
+extern "C" int pcub_abi_version(void) { return 2; }
 
 // Tuning hooks (not part of the stable ABI): choose / describe the decode kernel variant.
 extern "C" int pcub_sc_num_variants(void) { return kNumVariants; }

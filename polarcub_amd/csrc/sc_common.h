@@ -186,11 +186,16 @@ PCUB_HD uint64_t gather_stride(uint64_t x) {
         x = (x | (x >> 7)) & 0x0003000300030003ull;
         x = (x | (x >> 14)) & 0x0000000F0000000Full;
         return (x | (x >> 28)) & 0x00000000000000FFull;
-    } else {
-        static_assert(G == 16, "lanes per codeword");
+    } else if constexpr (G == 16) {
         x &= 0x0001000100010001ull;
         x = (x | (x >> 15)) & 0x0000000300000003ull;
         return (x | (x >> 30)) & 0x000000000000000Full;
+    } else if constexpr (G == 32) {
+        x &= 0x0000000100000001ull;
+        return (x | (x >> 31)) & 0x3ull;
+    } else {
+        static_assert(G == 64, "lanes per codeword");
+        return x & 1ull;
     }
 }
 

@@ -1,0 +1,449 @@
+// sc_del_kern.h -- SC decoding over the deletion channel (collection of binary
+// trellises): the kernel template (gfx950).  Instantiated per trellis length in
+// sc_del_n*.hip; sc_del.hip owns the C-ABI launcher.
+//
+// Replaces BinaryPolarEncoderDecoder.decode (BinaryPolarEncoderDecoder.py:71-99,
+// recursion :223-325) when the xy vector distribution is the
+// CollectionOfBinaryTrellises built by
+// buildCollectionOfBinaryTrellises_uniformInput_deletion
+// (VectorDistributions/CollectionOfBinaryTrellises.py:106-129) from a received
+// word, for a batch of received words.
+//
+// Geometry.  T = 2^(n-n0) trellises per codeword -> T lanes per codeword (one
+// trellis per lane; T <= 256, i.e. at most one workgroup), 256/T codewords per
+// 256-thread workgroup.  Lane position p (lane & (T-1)) owns trellis bitrev(p).
+// Everything above depth n0 -- the trellis levels -- is lane-local: the plus
+// transform of trellis t needs only t's slice of the minus child's re-encoded
+// vector (CollectionOfBinaryTrellises.py:58-66), and the re-encoding combine
+// (BinaryPolarEncoderDecoder.py:319-323) maps trellis t's slices onto itself.  At
+// depth n0 the length-1 trellises collapse to the rows of a memoryless node of
+// length T (one compact value per lane, half-split order because lane position p
+// owns trellis bitrev(p)), decoded by the binary kernel's machinery:
+//   * T <= 32: across the codeword's lanes (XSub<T>, sc_bin_body.h);
+//   * T >= 64: the workgroup's 256 collapsed values go through LDS to wave 0, which
+//     decodes every codeword of the group at once with 64/CPB lanes per codeword and
+//     4 values per lane (WinTree<4, 64/CPB, T/64>: the binary kernel's register
+//     subtree, lane-local top levels + XSub), and hands back the encoding bits and
+//     decisions through LDS.
+//
+// n0 = 2 without guard-band ones (main_deletion.py's default shape at n = 8) runs on
+// the register-resident representation of trellis_n02.h (no per-lane memory at
+// all); other shapes keep one trellis per depth (the current SC path) in private
+// memory (trellis_body.h), with capacities for up to OC guard-band ones.  The
+// schedule is identical in every lane, only trip counts of the small edge loops
+// differ.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "polarcub_sc.h"
+#include "sc_bin_body.h"
+#include "trellis_body.h"
+#include "trellis_n02.h"
+
+namespace pcub {
+
+constexpr int kDelBlock = 256;
+
+struct DelArgs {
+    const uint8_t* rx;      // [B][stride] received symbols (0/1)
+    const int32_t* rx_len;  // [B]
+    long long B;
+    int stride;
+    int n;
+    double pd;
+    OnesProbs op;           // guard-band ones and their vertex probabilities
+    const uint32_t* fmask;
+    const uint32_t* fval;
+    uint32_t* info;         // [ceil(K/32)][B] or null
+    uint32_t* xhat;         // [ceil(N/32)][B] or null
+    const uint32_t* fval_cw;  // [ceil(N/32)][B] per-codeword frozen values (export mode), or null
+    double* leaf;           // [N][B] compact normalised leaves (export mode)
+    int rw;                 // > 0: words per codeword of the bit-packed received words in LDS
+};
+
+// XSub (sc_bin_body.h) for the export mode: no rate-0 node is skipped and the two
+// normalised leaves of every M = 2 node are written (by group position 0) at
+// leaf[u * B] -- the xy marginals the genie reads (BinaryPolarEncoderDecoder.py:268-273).
+template <int M, int UBASE>
+struct XSubE {
+    __device__ static uint32_t run(double v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane, double* leaf,
+                                   long long B, bool store) {
+        const double w = xor_shfl_c<M / 2>(v);
+        const bool lo = (lane & (M / 2)) == 0;
+        const double a = lo ? v : w, b = lo ? w : v;
+        if constexpr (M == 2) {
+            const double c0 = op_f(a, b);
+            const uint32_t u0 = ((fm >> UBASE) & 1u) ? (uint32_t)((fv >> UBASE) & 1u) : leaf_v(c0);
+            const double c1 = op_g(a, b, u0);
+            const uint32_t u1 = ((fm >> (UBASE + 1)) & 1u) ? (uint32_t)((fv >> (UBASE + 1)) & 1u) : leaf_v(c1);
+            if (store) {
+                leaf[(long long)UBASE * B] = c0;
+                leaf[(long long)(UBASE + 1) * B] = c1;
+            }
+            ub |= ((uint64_t)u0 << UBASE) | ((uint64_t)u1 << (UBASE + 1));
+            return lo ? (u0 ^ u1) : u1;
+        } else {
+            constexpr int H = M / 2;
+            const uint32_t ym = XSubE<H, UBASE>::run(op_f(a, b), ub, fm, fv, lane, leaf, B, store);
+            const uint32_t yp = XSubE<H, UBASE + H>::run(op_g(a, b, ym), ub, fm, fv, lane, leaf, B, store);
+            return lo ? (ym ^ yp) : yp;
+        }
+    }
+};
+
+// Per-lane decoding context: frozen windows, decisions, information accumulator.
+template <int T, bool EXP>
+struct DelCtx {
+    static constexpr int NW = T > 64 ? T / 64 : 1;  // 64-bit windows of a memoryless subtree
+    static constexpr int CPB = kDelBlock / T;       // codewords per workgroup
+    static constexpr int GL = 64 / (CPB < 64 ? CPB : 64);  // wave-0 lanes per codeword (T >= 64)
+    DelArgs A;  // by value: taking the kernel argument's address would force it to scratch
+    long long cw;
+    bool leader;  // group position 0 stores the information words and exported leaves
+    int lane;
+    int k;        // next memoryless subtree (u range [k*T, (k+1)*T))
+    uint32_t acc;
+    int nacc;
+    int infow;
+    // T >= 64, decode mode: exchange buffers in LDS (see subtree())
+    double* xv;               // [256] collapsed values, codeword g's at [g*T, (g+1)*T)
+    unsigned long long* xb;   // [4] ballots of the encoding bits, one per local index
+    unsigned long long* xub;  // [CPB][NW] decisions per codeword
+
+    // bits [k*T + 64w, ...) of a bit vector whose word i is w[i * stride]
+    PCUB_HD uint64_t window(const uint32_t* w, int wi, long long stride = 1) const {
+        const int us = k * T + 64 * wi;
+        if constexpr (T >= 64) {
+            return (uint64_t)w[(us >> 5) * stride] | ((uint64_t)w[((us >> 5) + 1) * stride] << 32);
+        } else {
+            return (uint64_t)((w[(us >> 5) * stride] >> (us & 31)) & (uint32_t)((1ull << T) - 1ull));
+        }
+    }
+
+    // SC over the collapsed memoryless node (one compact value per lane); returns
+    // this lane's bit of the node's re-encoded vector (natural position = its trellis).
+    __device__ __forceinline__ uint32_t subtree(double v) {
+        uint64_t fm[NW], fv[NW], ub[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            fm[w] = window(A.fmask, w);
+            fv[w] = A.fval_cw ? window(A.fval_cw + cw, w, A.B) : window(A.fval, w);
+            ub[w] = 0;
+        }
+        uint32_t y;
+        constexpr uint64_t WM = (T >= 64) ? ~0ull : ((1ull << T) - 1ull);
+        bool rate0 = true;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) rate0 = rate0 && (fm[w] == WM);
+        if constexpr (EXP) {
+            static_assert(T <= 64, "export mode: at most 64 trellises");
+            y = XSubE<T, 0>::run(v, ub[0], fm[0], fv[0], lane, A.leaf + (long long)k * T * A.B + cw, A.B, leader) & 1u;
+        } else if (rate0) {  // rate-0 node: decisions are the frozen values
+#pragma unroll
+            for (int w = 0; w < NW; ++w) ub[w] = fv[w];
+            const int p = threadIdx.x & (T - 1);
+            if constexpr (T <= 64) y = frozen_local<1, T>(fv[0], p);
+            else y = frozen_bit_wide(fv, p);
+        } else if constexpr (T >= 64) {
+            // One codeword per wave (or per workgroup) is the trellis stages' layout, but
+            // a length-T subtree decoded across all those lanes spends a full wave op on
+            // every node.  So the group's collapsed rows go through LDS to wave 0, which
+            // decodes them all at once with GL lanes per codeword, 4 values per lane (lane
+            // j of group c owns positions j + GL*t: the binary kernel's register subtree),
+            // and hands back the encoding bits and decisions.  fm / fv are the same for
+            // the whole group (per-codeword frozen values exist only in export mode), so
+            // every wave takes this branch together.
+            const int wv = threadIdx.x >> 6;
+            xv[threadIdx.x] = v;
+            __syncthreads();
+            // (measured at T = 64: wave 0 with four codewords beats two waves with two
+            // each, and beats rotating the decoding wave over the group's waves)
+            if (wv == 0) {
+                const int c = lane / GL, j = lane % GL;
+                double vv[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) vv[t] = xv[c * T + j + GL * t];
+                uint64_t ubl[NW];
+#pragma unroll
+                for (int w = 0; w < NW; ++w) ubl[w] = 0;
+                const uint32_t bits = WinTree<4, GL, NW>::run(vv, ubl, fm, fv, lane);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const unsigned long long bal = __ballot((bits >> t) & 1u);
+                    if (lane == 0) xb[t] = bal;
+                }
+                if (j == 0)
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) xub[c * NW + w] = ubl[w];
+            }
+            __syncthreads();
+            // position p of codeword g is local index p / GL of wave-0 lane g*GL + p % GL
+            const int p = threadIdx.x & (T - 1);
+            const int g = threadIdx.x / T;
+            y = (uint32_t)(xb[p / GL] >> (g * GL + p % GL)) & 1u;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) ub[w] = xub[g * NW + w];
+        } else {
+            y = XSub<T, 0>::run(v, ub[0], fm[0], fv[0], lane) & 1u;
+        }
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            for (uint64_t im = ~fm[w] & WM; im != 0ull; im &= im - 1ull) {
+                acc |= (uint32_t)((ub[w] >> __builtin_ctzll(im)) & 1ull) << nacc;
+                if (++nacc == 32) {
+                    if (leader && A.info) A.info[(long long)infow * A.B + cw] = acc;
+                    acc = 0;
+                    nacc = 0;
+                    ++infow;
+                }
+            }
+        }
+        ++k;
+        return y;
+    }
+
+    // bit p of the polar transform (re-encoding) of NW*64 known bits fv (rate-0 node, T > 64)
+    PCUB_HD uint32_t frozen_bit_wide(const uint64_t* fv, int p) const {
+        // the encoding of a node is [enc(left) ^ enc(right) | enc(right)] over its halves:
+        // fold the windows from the top
+        uint64_t e[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) e[w] = polar_bits(fv[w]);
+#pragma unroll
+        for (int h = 1; h < NW; h <<= 1)
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+                if ((w & h) == 0) e[w] ^= e[w + h];
+        uint64_t sel = e[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) sel = ((p >> 6) == w) ? e[w] : sel;
+        return (uint32_t)((sel >> (p & 63)) & 1ull);
+    }
+};
+
+// The collapse of a length-2 trellis (CollectionOfBinaryTrellises.py:68-82) into the
+// row of the memoryless node: without guard-band ones by trellis_collapse (no child
+// built), with ones by building the length-1 child and taking its marginal.
+template <int L, int OC, class PT>
+__device__ __forceinline__ void del_collapse(const PT& t, const uint32_t* dec, int ones, double& m0, double& m1) {
+    if constexpr (OC > 0) {
+        if (ones > 0) {
+            using Cap = DelCap<L, OC>;
+            constexpr int d = (L == 2) ? 1 : (L == 4) ? 2 : (L == 8) ? 3 : 4;
+            Trel<1, Cap::V, Cap::E(d)> c;
+            trellis_transform<2>(t, c, dec);
+            trellis_marginal(c, m0, m1);
+            return;
+        }
+    }
+    trellis_collapse(t, dec, m0, m1);
+}
+
+// One SC node of the trellis levels: trellis `t` of length LEN (this lane's
+// slice of the collection).  Returns the node's re-encoded slice, natural order.
+template <int L, int T, int LEN, bool EXP, int OC>
+struct DelNode {
+    template <class PT>
+    __device__ static uint32_t run(const PT& t, DelCtx<T, EXP>& cx) {
+        using Cap = DelCap<L, OC>;
+        if constexpr (LEN == 2) {
+            // children are length-1 trellises collapsed to memoryless rows
+            // (CollectionOfBinaryTrellises.py:68-82), then normalised by the decoder
+            double m0, m1;
+            del_collapse<L, OC>(t, nullptr, cx.A.op.ones, m0, m1);
+            const uint32_t xm = cx.subtree(norm_pack(m0, m1));
+            del_collapse<L, OC>(t, &xm, cx.A.op.ones, m0, m1);
+            const uint32_t xp = cx.subtree(norm_pack(m0, m1));
+            return (xm ^ xp) | (xp << 1);
+        } else {
+            constexpr int H = LEN / 2;
+            constexpr int d = (L / H == 2) ? 1 : (L / H == 4) ? 2 : (L / H == 8) ? 3 : 4;  // child depth
+            Trel<H, Cap::V, Cap::E(d)> c;
+            trellis_transform<LEN>(t, c, nullptr);
+            trellis_normalize<H>(c);
+            const uint32_t ym = DelNode<L, T, H, EXP, OC>::run(c, cx);
+            trellis_transform<LEN>(t, c, &ym);
+            trellis_normalize<H>(c);
+            const uint32_t yp = DelNode<L, T, H, EXP, OC>::run(c, cx);
+            uint32_t x = 0;  // x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h]
+#pragma unroll
+            for (int h = 0; h < H; ++h)
+                x |= ((((ym ^ yp) >> h) & 1u) << (2 * h)) | (((yp >> h) & 1u) << (2 * h + 1));
+            return x;
+        }
+    }
+};
+
+// n0 = 2: the two trellis levels on the register-resident representation
+// (trellis_n02.h); same recursion as DelNode.  Returns the 4-bit re-encoded slice.
+// one depth-1 node: minus (dec == nullptr) or plus child of the base trellis
+template <int T, bool EXP>
+__device__ __forceinline__ uint32_t del_n02_half(const Base02& b, const uint32_t* dec, DelCtx<T, EXP>& cx) {
+    Child02 c;
+    n02_transform(b, dec, c);
+    n02_normalize(c);
+    double m0, m1;
+    n02_collapse(c, nullptr, m0, m1);
+    const uint32_t xm = cx.subtree(norm_pack(m0, m1));
+    n02_collapse(c, &xm, m0, m1);
+    const uint32_t xp = cx.subtree(norm_pack(m0, m1));
+    return (xm ^ xp) | (xp << 1);
+}
+
+template <int T, bool EXP>
+__device__ __forceinline__ uint32_t del_n02(const Base02& b, DelCtx<T, EXP>& cx) {
+    const uint32_t ym = del_n02_half(b, nullptr, cx);
+    const uint32_t yp = del_n02_half(b, &ym, cx);
+    uint32_t x = 0;  // x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h]
+#pragma unroll
+    for (int h = 0; h < 2; ++h) x |= ((((ym ^ yp) >> h) & 1u) << (2 * h)) | (((yp >> h) & 1u) << (2 * h + 1));
+    return x;
+}
+
+template <int N0, int TB, bool EXP, int OC>
+__global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
+    constexpr int L = 1 << N0;
+    constexpr int T = 1 << TB;
+    constexpr int CPB = kDelBlock / T;       // codewords per workgroup
+    constexpr int NB = T * L;                // code length N
+    constexpr int WPC = (NB + 31) / 32;      // x_hat words per codeword
+    using Cap = DelCap<L, OC>;
+    static_assert(T <= kDelBlock, "at most one workgroup per codeword");
+    __shared__ uint32_t xs[CPB * WPC];
+
+    const int lane = threadIdx.x & 63;
+    const int p = threadIdx.x & (T - 1);
+    const int g = threadIdx.x >> TB;
+    const long long cw = (long long)blockIdx.x * CPB + g;
+    const bool valid = cw < A.B;
+    const long long c = valid ? cw : A.B - 1;  // padding groups decode a duplicate, store nothing
+    for (int i = threadIdx.x; i < CPB * WPC; i += kDelBlock) xs[i] = 0;
+
+    // Received words, bit-packed into LDS (rw > 0, the launcher's choice when the
+    // group's words fit): each wave packs whole codewords with coalesced byte loads
+    // and a ballot per 64 symbols, so the guard-band parse below probes 32 symbols
+    // per LDS read instead of walking zero runs one dependent global load at a time.
+    extern __shared__ uint32_t rxb[];
+    const bool pk = A.rw > 0;
+    if (pk) {
+        for (int gg = threadIdx.x >> 6; gg < CPB; gg += kDelBlock / 64) {
+            long long cg = (long long)blockIdx.x * CPB + gg;
+            cg = cg < A.B ? cg : A.B - 1;
+            const uint8_t* row = A.rx + cg * (long long)A.stride;
+            int ln = A.rx_len[cg];
+            ln = ln < 0 ? 0 : (ln > A.stride ? A.stride : ln);
+            for (int base = 0; base < A.rw * 32; base += 64) {
+                const int i = base + lane;
+                const unsigned long long msk = __ballot(i < ln && row[i] == 1);
+                const int wi = (base >> 5) + (lane & 1);
+                if (lane < 2 && wi < A.rw) rxb[gg * A.rw + wi] = (uint32_t)(msk >> (32 * lane));
+            }
+        }
+        __syncthreads();
+    }
+
+    const uint8_t* w = A.rx + c * (long long)A.stride;
+    const uint32_t* pw = rxb + (pk ? g * A.rw : 0);
+    int len = A.rx_len[c];
+    len = len < 0 ? 0 : (len > A.stride ? A.stride : len);
+    auto bit = [w, pw, pk](int i) { return pk ? (int)((pw[i >> 5] >> (i & 31)) & 1u) : (int)w[i]; };
+    const int t = (int)bitrev((uint32_t)p, TB);
+    int s, m;
+    if (pk) segment_of_packed(pw, len, TB, t, s, m);
+    else segment_of(bit, len, TB, t, s, m);
+
+    __shared__ double xv[(T >= 64 && !EXP) ? kDelBlock : 1];
+    __shared__ unsigned long long xb[4], xub[(T >= 64 && !EXP) ? CPB * DelCtx<T, EXP>::NW : 1];
+    DelCtx<T, EXP> cx;
+    cx.xv = xv;
+    cx.xb = xb;
+    cx.xub = xub;
+    cx.A = A;
+    cx.cw = cw;
+    cx.leader = valid && p == 0;
+    cx.lane = lane;
+    cx.k = 0;
+    cx.acc = 0;
+    cx.nacc = 0;
+    cx.infow = 0;
+    uint32_t x;
+    if constexpr (N0 == 2 && OC == 0) {
+        // register-resident path (trellis_n02.h): the base trellis is implicit
+        Base02 b;
+        b.m = m;
+        b.d = kN02L - m;
+        b.y = 0;
+        if (m <= kN02L)
+            for (int i = 0; i < m; ++i) b.y |= (uint32_t)(bit(s + i) & 1) << i;
+        b.pins = 0.5 * (1.0 - A.pd);
+        b.pdel = 0.5 * A.pd;
+        x = del_n02(b, cx);
+    } else {
+        Trel<L, Cap::V, Cap::E0> base;
+        trellis_build<L>(base, bit, s, m, A.pd, A.op);
+        x = DelNode<L, T, L, EXP, OC>::run(base, cx);
+    }
+    if (cx.nacc && cx.leader && A.info) A.info[(long long)cx.infow * A.B + cw] = cx.acc;
+
+    // x_hat: trellis t's slice is natural positions [t*L, (t+1)*L)
+    __syncthreads();
+    const int pos = t * L;
+    atomicOr(&xs[g * WPC + (pos >> 5)], (x & (uint32_t)((1ull << L) - 1ull)) << (pos & 31));
+    __syncthreads();
+    if (A.xhat && valid)
+        for (int i = p; i < WPC; i += T) A.xhat[(long long)i * A.B + cw] = xs[g * WPC + i];
+}
+
+typedef void (*DelKern)(DelArgs);
+
+// the kernel for (n0, n - n0) trellis shape, export mode, guard-band-ones capacity; or nullptr
+DelKern del_kernel_n1(int tb, bool exp, int oc);
+DelKern del_kernel_n2(int tb, bool exp, int oc);
+DelKern del_kernel_n3(int tb, bool exp, int oc);
+DelKern del_kernel_n4(int tb, bool exp, int oc);
+
+// decode mode: T up to 256 (one workgroup), OC 0 or 3; export mode: T <= 64, OC 0
+template <int N0>
+DelKern del_kernel_tb(int tb, bool exp, int oc) {
+    if (exp) {
+        if (oc != 0) return nullptr;
+        switch (tb) {
+            case 1: return k_sc_del<N0, 1, true, 0>;
+            case 2: return k_sc_del<N0, 2, true, 0>;
+            case 3: return k_sc_del<N0, 3, true, 0>;
+            case 4: return k_sc_del<N0, 4, true, 0>;
+            case 5: return k_sc_del<N0, 5, true, 0>;
+            case 6: return k_sc_del<N0, 6, true, 0>;
+            default: return nullptr;
+        }
+    }
+    if (oc == 0) {
+        switch (tb) {
+            case 1: return k_sc_del<N0, 1, false, 0>;
+            case 2: return k_sc_del<N0, 2, false, 0>;
+            case 3: return k_sc_del<N0, 3, false, 0>;
+            case 4: return k_sc_del<N0, 4, false, 0>;
+            case 5: return k_sc_del<N0, 5, false, 0>;
+            case 6: return k_sc_del<N0, 6, false, 0>;
+            case 7: return k_sc_del<N0, 7, false, 0>;
+            case 8: return k_sc_del<N0, 8, false, 0>;
+            default: return nullptr;
+        }
+    }
+    if (oc == 3) {
+        switch (tb) {
+            case 1: return k_sc_del<N0, 1, false, 3>;
+            case 2: return k_sc_del<N0, 2, false, 3>;
+            case 3: return k_sc_del<N0, 3, false, 3>;
+            case 4: return k_sc_del<N0, 4, false, 3>;
+            case 5: return k_sc_del<N0, 5, false, 3>;
+            case 6: return k_sc_del<N0, 6, false, 3>;
+            case 7: return k_sc_del<N0, 7, false, 3>;
+            case 8: return k_sc_del<N0, 8, false, 3>;
+            default: return nullptr;
+        }
+    }
+    return nullptr;
+}
+
+}  // namespace pcub

@@ -7,8 +7,8 @@
 //   BinaryTrellis.calcNormalizationVector / normalize         VectorDistributions/BinaryTrellis.py:280-306
 //   BinaryTrellis.calcMarginalizedProbabilities(normalize=False), as called by the
 //   collection collapse                                      VectorDistributions/CollectionOfBinaryTrellises.py:68-82
-// for a single-state, uniform-input trellis with no guard-band ones
-// (numberOfOnesToAddAtBothEndsOfGuardbands = 0, the main_deletion.py default).
+// for a single-state, uniform-input trellis, with or without guard-band ones
+// (numberOfOnesToAddAtBothEndsOfGuardbands; main_deletion.py's default is 0).
 //
 // Order of floating-point sums.  The reference keeps vertices and edges in
 // insertion-ordered dicts and every sum (edge accumulation in a transform, the
@@ -19,13 +19,17 @@
 // in insertion order.  Iterating "vertices of layer i in order, then the edge
 // array filtered by from-vertex" is then the reference's iteration, and all
 // sums are formed in the same order (tests/test_trellis_* pin this bit-exactly).
+// Vertex probabilities matter only on the first and last layer (the marginal of a
+// length-1 trellis, :260-278); they are kept for those two layers.
 //
-// Capacities (ones = 0).  Base layer l of a trellis of length L with m received
-// symbols holds vpos in [max(0, l - (L - m)), min(l, m)]: at most L/2 + 1
-// vertices.  A transformed trellis's layer j is a subset of base layer j*2^d, so
-// every layer of every depth has at most V = L/2 + 1 vertices; a base edge layer
-// has at most 3V edges (one insertion, two deletions per vertex) and a
-// transformed one at most 2*V*V (one per (from, to, label)).
+// Capacities (OC = the most guard-band ones the instantiation accepts).  Base layer
+// l of a trellis of length L with m received symbols and `ones` ones holds vpos in
+// [max(0, l + ones - dc), min(l + ones, m)], dc = L + 2 ones - m: at most
+// V = L/2 + 1 + ones vertices.  A transformed trellis's layer j is a subset of base
+// layer j*2^d, so every layer of every depth has at most V vertices; a base edge
+// layer has at most 3V edges (one insertion, two deletions per vertex) and an edge of
+// a depth-d trellis spans 2^d base layers, so it advances vpos by 0 .. 2^d: at most
+// 2V(2^d + 1) edges (one per from-vertex, advance, label), and never more than 2V^2.
 #pragma once
 #include "sc_common.h"
 
@@ -41,7 +45,9 @@ template <int LEN, int V, int E>
 struct Trel {
     int8_t nv[LEN + 1];     // vertices per layer
     int16_t vp[LEN + 1][V]; // vpos in insertion order
-    int8_t ne[LEN];         // edges per edge layer
+    double pr0[V];          // vertex probabilities of layer 0 (insertion order)
+    double prL[V];          // ... and of layer LEN
+    int16_t ne[LEN];        // edges per edge layer
     uint32_t key[LEN][E];   // creation order
     double p[LEN][E];
 
@@ -49,13 +55,25 @@ struct Trel {
         for (int l = 0; l <= LEN; ++l) nv[l] = 0;
         for (int l = 0; l < LEN; ++l) ne[l] = 0;
     }
-    // __getVertexAndAddIfNeeded (BinaryTrellis.py:155-162)
-    PCUB_HD void vertex(int l, int vpos) {
+    // __getVertexAndAddIfNeeded (BinaryTrellis.py:155-162); returns the vertex's index
+    PCUB_HD int vertex(int l, int vpos) {
         const int c = nv[l];
         for (int i = 0; i < c; ++i)
-            if (vp[l][i] == vpos) return;
+            if (vp[l][i] == vpos) return i;
         vp[l][c] = (int16_t)vpos;
         nv[l] = (int8_t)(c + 1);
+        return c;
+    }
+    // setVertexProb (BinaryTrellis.py:123-125), first / last layer
+    PCUB_HD void set_prob(int l, int vpos, double prob) {
+        const int i = vertex(l, vpos);
+        if (l == 0) pr0[i] = prob;
+        else prL[i] = prob;
+    }
+    PCUB_HD double prob_last(int vpos) const {
+        for (int i = 0; i < nv[LEN]; ++i)
+            if (vp[LEN][i] == vpos) return prL[i];
+        return 1.0;
     }
     // addToEdgeProb (BinaryTrellis.py:128-136): from-vertex, to-vertex, then the edge (+= p)
     PCUB_HD void add(int l, int u, int v, int x, double prob) {
@@ -70,31 +88,51 @@ struct Trel {
             }
         key[l][c] = k;
         p[l][c] = 0.0 + prob;
-        ne[l] = (int8_t)(c + 1);
+        ne[l] = (int16_t)(c + 1);
     }
 };
 
-template <int L>
-struct TrelCap {
-    static constexpr int V = L / 2 + 1;
+// capacities of the trellises of base length L accepting up to OC guard-band ones
+template <int L, int OC = 0>
+struct DelCap {
+    static constexpr int V = L / 2 + 1 + OC;
+    static constexpr int E0 = 3 * V;  // base edge layer
+    // edge layer of a depth-d trellis (d >= 1)
+    static constexpr int E(int d) { return 2 * V * V < 2 * V * ((1 << d) + 1) ? 2 * V * V : 2 * V * ((1 << d) + 1); }
+};
+
+// Guard-band vertex probabilities, comb(ones, i) (1-pd)^i pd^(ones-i) for i = 0 .. ones
+// (buildTrellis_uniformInput_deletion, BinaryTrellis.py:343-345, 371-373), computed on the
+// host with libm pow -- the function CPython's float ** int calls -- so they are the
+// reference's values bit for bit.
+struct OnesProbs {
+    int ones;
+    double pr[4];
 };
 
 // The base trellis of one segment, word[s .. s+m) (buildTrellis_uniformInput_deletion,
-// ones = 0, trimmed edges).  `bit(i)` returns received symbol i of the codeword.
+// trimmed edges, op.ones guard-band ones).  `bit(i)` returns received symbol i of the codeword.
 template <int L, class T, class BitF>
-PCUB_HD void trellis_build(T& t, const BitF& bit, int s, int m, double pd) {
+PCUB_HD void trellis_build(T& t, const BitF& bit, int s, int m, double pd, const OnesProbs& op = OnesProbs{0, {1.0}}) {
     t.clear();
-    const int dcount = L - m;
-    t.vertex(0, 0);  // setVertexProb: start vertex, prob 1.0
-    t.vertex(L, m);  // end vertex, prob 1.0
+    const int ones = op.ones;
+    const int dcount = L + 2 * ones - m;
+    if (ones > 0) {
+        const int k = ones < m ? ones : m;
+        for (int i = 0; i <= k; ++i) t.set_prob(0, i, op.pr[i]);
+        for (int i = m; i >= m - k; --i) t.set_prob(L, i, op.pr[m - i]);
+    } else {
+        t.set_prob(0, 0, 1.0);  // setVertexProb: start vertex, prob 1.0
+        t.set_prob(L, m, 1.0);  // end vertex, prob 1.0
+    }
     const double p_ins = 0.5 * (1.0 - pd);
     const double p_del = 0.5 * pd;
     for (int l = 0; l < L; ++l) {
-        const int lo = l - dcount > 0 ? l - dcount : 0;
-        const int hi = l < m ? l : m;
+        const int lo = l + ones - dcount > 0 ? l + ones - dcount : 0;
+        const int hi = l + ones < m ? l + ones : m;
         for (int vp = lo; vp <= hi; ++vp) {
             if (vp < m) t.add(l, vp, vp + 1, bit(s + vp), p_ins);
-            if (l + 1 - dcount <= vp) {
+            if (l + 1 + ones - dcount <= vp) {
                 // label 0 then 1; a deletion of a 0 at either trimmed edge is certain
                 t.add(l, vp, vp, 0, (vp > 0 && vp < m) ? p_del : 0.5);
                 t.add(l, vp, vp, 1, p_del);
@@ -109,8 +147,8 @@ template <int LEN, class P, class C>
 PCUB_HD void trellis_transform(const P& pt, C& ct, const uint32_t* dec) {
     constexpr int H = LEN / 2;
     ct.clear();
-    for (int i = 0; i < pt.nv[0]; ++i) ct.vertex(0, pt.vp[0][i]);
-    for (int i = 0; i < pt.nv[LEN]; ++i) ct.vertex(H, pt.vp[LEN][i]);
+    for (int i = 0; i < pt.nv[0]; ++i) ct.set_prob(0, pt.vp[0][i], pt.pr0[i]);
+    for (int i = 0; i < pt.nv[LEN]; ++i) ct.set_prob(H, pt.vp[LEN][i], pt.prL[i]);
     for (int j = 0; j < H; ++j) {
         const int mid = 2 * j + 1;
         const int dj = dec ? (int)((*dec >> j) & 1u) : 0;
@@ -157,25 +195,28 @@ PCUB_HD void trellis_normalize(T& t) {
 }
 
 // calcMarginalizedProbabilities(normalize=False) of a length-1 trellis
-// (BinaryTrellis.py:260-278): vertexProb * edgeProb * toVertex.vertexProb / 1.0,
-// all vertex probabilities 1.0 when ones = 0, so each term is the edge probability.
+// (BinaryTrellis.py:260-278): vertexProb * edgeProb * toVertex.vertexProb / 1.0 summed
+// per label, vertices in order, out-edges in creation order.
 template <class T>
 PCUB_HD void trellis_marginal(const T& t, double& m0, double& m1) {
     m0 = 0.0;
     m1 = 0.0;
     for (int vi = 0; vi < t.nv[0]; ++vi) {
         const int v = t.vp[0][vi];
+        const double pv = t.pr0[vi];
         for (int e = 0; e < t.ne[0]; ++e) {
             const uint32_t k = t.key[0][e];
             if (ek_from(k) != v) continue;
-            if (ek_lbl(k)) m1 += t.p[0][e];
-            else m0 += t.p[0][e];
+            const double term = pv * t.p[0][e] * t.prob_last(ek_to(k));
+            if (ek_lbl(k)) m1 += term;
+            else m0 += term;
         }
     }
 }
 
-// The collapse of a length-2 trellis (CollectionOfBinaryTrellises.py:68-82): its
-// minus/plus child has length 1, and with no guard-band ones its only vertices are
+// The collapse of a length-2 trellis (CollectionOfBinaryTrellises.py:68-82) with no
+// guard-band ones (every vertex probability 1.0): its minus/plus child has length 1,
+// and its only vertices are
 // the start (vpos 0) and the end (vpos m), so the child has at most two edges,
 // start -> end with label 0 and with label 1.  The child's marginal (normalize=False)
 // is therefore 0.0 + the accumulated probability of each of those edges, i.e. the

@@ -90,7 +90,7 @@ def awgn_batch(code, B, sigma2, generator, chunk=1 << 18):
     return xy, info
 
 
-def deletion_batch(code, B, n0, xi, pd, generator, chunk=1 << 17):
+def deletion_batch(code, B, n0, xi, pd, generator, chunk=1 << 17, ones=0):
     """Uniform information -> GPU encoder -> guard bands -> deletion channel.
     Returns (rx [B, W] uint8, rx_len [B] int32, info [B, K] uint8)."""
     dev = code.device
@@ -99,7 +99,7 @@ def deletion_batch(code, B, n0, xi, pd, generator, chunk=1 << 17):
         b1 = min(B, b0 + chunk)
         inf = torch.randint(0, 2, (b1 - b0, code.K), dtype=torch.uint8, device=dev, generator=generator)
         x = sc.encode(code, inf)
-        rx, ln = channel.deletion_words(x, code.n, n0, xi, pd, generator=generator)
+        rx, ln = channel.deletion_words(x, code.n, n0, xi, pd, generator=generator, ones=ones)
         rxs.append(rx)
         lens.append(ln)
         infos.append(inf)

@@ -362,22 +362,29 @@ def encode_qary(code, info):
     return x.t().contiguous()
 
 
-def deletion_supported(n, n0):
-    """True when pcub_sc_decode_deletion has a kernel for 2^n0-input trellises and 2^(n-n0) of them."""
-    return bool(_lib.lib().pcub_sc_deletion_supported(int(n), int(n0)))
+def deletion_supported(n, n0, ones=0):
+    """True when pcub_sc_decode_deletion has a kernel for 2^(n-n0) trellises of 2^n0 inputs
+    with `ones` guard-band ones."""
+    return bool(_lib.lib().pcub_sc_deletion_supported(int(n), int(n0), int(ones)))
+
+
+def leaf_deletion_supported(n, n0, ones=0):
+    """True when pcub_sc_leaf_deletion (every leaf exported: the genie) covers the shape."""
+    return bool(_lib.lib().pcub_sc_leaf_deletion_supported(int(n), int(n0), int(ones)))
 
 
 class DeletionDecoder:
     """Batched SC decoder over the deletion channel (CollectionOfBinaryTrellises built from
-    each received word with buildCollectionOfBinaryTrellises_uniformInput_deletion, no
-    guard-band ones) for one CodeSpec."""
+    each received word with buildCollectionOfBinaryTrellises_uniformInput_deletion, with
+    `ones` guard-band ones) for one CodeSpec."""
 
-    def __init__(self, code, n0, pd):
+    def __init__(self, code, n0, pd, ones=0):
         self.code = code
         self.n0 = int(n0)
         self.pd = float(pd)
-        if not deletion_supported(code.n, self.n0):
-            raise ValueError("no deletion kernel for n=%d, n0=%d" % (code.n, self.n0))
+        self.ones = int(ones)
+        if not deletion_supported(code.n, self.n0, self.ones):
+            raise ValueError("no deletion kernel for n=%d, n0=%d, ones=%d" % (code.n, self.n0, self.ones))
 
     def decode_native(self, rx, rx_len, want_xhat=True):
         """rx: [B, W] uint8 received symbols on device, rx_len: [B] int32.
@@ -392,8 +399,8 @@ class DeletionDecoder:
             raise ValueError("rx_len must have B entries")
         info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=rx.device)
         xh = torch.empty((c.n_words, B), dtype=torch.int32, device=rx.device) if want_xhat else None
-        rc = _lib.lib().pcub_sc_decode_deletion(_p(rx), _p(ln), B, W, c.n, self.n0, self.pd, _p(c.fmask_dev),
-                                                _p(c.fval_dev), c.K, _p(info), _p(xh), _stream())
+        rc = _lib.lib().pcub_sc_decode_deletion(_p(rx), _p(ln), B, W, c.n, self.n0, self.ones, self.pd,
+                                                _p(c.fmask_dev), _p(c.fval_dev), c.K, _p(info), _p(xh), _stream())
         _lib.check(rc, "pcub_sc_decode_deletion")
         return info, xh
 
@@ -405,6 +412,8 @@ class DeletionDecoder:
     def decode_leaves(self, rx, rx_len, fval_cw=None):
         """Export mode (pcub_sc_leaf_deletion): (info [B, K], xhat [B, N], marginals [B, N, 2])."""
         c = self.code
+        if not leaf_deletion_supported(c.n, self.n0, self.ones):
+            raise ValueError("no leaf-export deletion kernel for n=%d, n0=%d, ones=%d" % (c.n, self.n0, self.ones))
         rx = rx.contiguous()
         B, W = rx.shape
         ln = rx_len.to(device=rx.device, dtype=torch.int32).contiguous()
@@ -412,8 +421,9 @@ class DeletionDecoder:
         info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=rx.device)
         xh = torch.empty((c.n_words, B), dtype=torch.int32, device=rx.device)
         leaf = torch.empty((c.N, B), dtype=torch.float64, device=rx.device)
-        rc = _lib.lib().pcub_sc_leaf_deletion(_p(rx), _p(ln), B, W, c.n, self.n0, self.pd, _p(c.fmask_dev),
-                                              _p(c.fval_dev), _p(fw), c.K, _p(info), _p(xh), _p(leaf), _stream())
+        rc = _lib.lib().pcub_sc_leaf_deletion(_p(rx), _p(ln), B, W, c.n, self.n0, self.ones, self.pd,
+                                              _p(c.fmask_dev), _p(c.fval_dev), _p(fw), c.K, _p(info), _p(xh),
+                                              _p(leaf), _stream())
         _lib.check(rc, "pcub_sc_leaf_deletion")
         return unpack(info, c.K), unpack(xh, c.N), leaf_marginals(leaf)
 

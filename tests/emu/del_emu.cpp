@@ -7,6 +7,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <cmath>
 #include <vector>
 
 #include "trellis_body.h"
@@ -48,59 +49,58 @@ std::vector<int> mem_sc(const std::vector<double>& v, Ctx& cx) {
     return x;
 }
 
-template <int L>
-struct Cap {
-    static constexpr int V = L / 2 + 1;
-    static constexpr int E0 = 3 * V;
-    static constexpr int E1 = 2 * V * V;
-};
+// the kernel's capacities: up to 3 guard-band ones when there are any (sc_del.hip)
+template <int L, int OC>
+using Cap = DelCap<L, OC>;
 
-template <int L, int LEN>
+template <int L>
+constexpr int depth_of(int len) {
+    return (L / len == 1) ? 0 : (L / len == 2) ? 1 : (L / len == 4) ? 2 : (L / len == 8) ? 3 : 4;
+}
+
+template <int L, int LEN, int OC>
 struct Node {
     template <class PT>
-    static std::vector<uint32_t> run(const std::vector<PT>& ts, Ctx& cx) {
+    static std::vector<uint32_t> run(const std::vector<PT>& ts, Ctx& cx, int ones) {
         const size_t T = ts.size();
         std::vector<uint32_t> out(T);
         if constexpr (LEN == 2) {
-            Trel<1, Cap<L>::V, Cap<L>::E1> c;
+            Trel<1, Cap<L, OC>::V, Cap<L, OC>::E(depth_of<L>(1))> c;
             std::vector<double> vals(T);
-            for (size_t t = 0; t < T; ++t) {
-                double m0, m1;
-                trellis_collapse(ts[t], nullptr, m0, m1);
-                // the materialised child gives the same marginal (kernel shortcut check)
-                double c0, c1;
-                trellis_transform<2>(ts[t], c, nullptr);
-                trellis_marginal(c, c0, c1);
-                if (as_bits(c0) != as_bits(m0) || as_bits(c1) != as_bits(m1)) throw 1;
-                vals[t] = norm_pack(m0, m1);
+            std::vector<int> xm;
+            for (int half = 0; half < 2; ++half) {
+                if (half) xm = mem_sc(vals, cx);
+                for (size_t t = 0; t < T; ++t) {
+                    const uint32_t d = half ? (uint32_t)xm[t] : 0u;
+                    double c0, c1;
+                    trellis_transform<2>(ts[t], c, half ? &d : nullptr);
+                    trellis_marginal(c, c0, c1);
+                    if (ones == 0) {  // the kernel's shortcut (no child built) must agree
+                        double m0, m1;
+                        trellis_collapse(ts[t], half ? &d : nullptr, m0, m1);
+                        if (as_bits(c0) != as_bits(m0) || as_bits(c1) != as_bits(m1)) throw 1;
+                    }
+                    vals[t] = norm_pack(c0, c1);
+                }
+                if (half) {
+                    const std::vector<int> xp = mem_sc(vals, cx);
+                    for (size_t t = 0; t < T; ++t) out[t] = (uint32_t)((xm[t] ^ xp[t]) | (xp[t] << 1));
+                }
             }
-            const std::vector<int> xm = mem_sc(vals, cx);
-            for (size_t t = 0; t < T; ++t) {
-                double m0, m1;
-                const uint32_t d = (uint32_t)xm[t];
-                trellis_collapse(ts[t], &d, m0, m1);
-                double c0, c1;
-                trellis_transform<2>(ts[t], c, &d);
-                trellis_marginal(c, c0, c1);
-                if (as_bits(c0) != as_bits(m0) || as_bits(c1) != as_bits(m1)) throw 1;
-                vals[t] = norm_pack(m0, m1);
-            }
-            const std::vector<int> xp = mem_sc(vals, cx);
-            for (size_t t = 0; t < T; ++t) out[t] = (uint32_t)((xm[t] ^ xp[t]) | (xp[t] << 1));
         } else {
             constexpr int H = LEN / 2;
-            using CT = Trel<H, Cap<L>::V, Cap<L>::E1>;
+            using CT = Trel<H, Cap<L, OC>::V, Cap<L, OC>::E(depth_of<L>(H))>;
             std::vector<CT> cs(T);
             for (size_t t = 0; t < T; ++t) {
                 trellis_transform<LEN>(ts[t], cs[t], nullptr);
                 trellis_normalize<H>(cs[t]);
             }
-            const std::vector<uint32_t> ym = Node<L, H>::run(cs, cx);
+            const std::vector<uint32_t> ym = Node<L, H, OC>::run(cs, cx, ones);
             for (size_t t = 0; t < T; ++t) {
                 trellis_transform<LEN>(ts[t], cs[t], &ym[t]);
                 trellis_normalize<H>(cs[t]);
             }
-            const std::vector<uint32_t> yp = Node<L, H>::run(cs, cx);
+            const std::vector<uint32_t> yp = Node<L, H, OC>::run(cs, cx, ones);
             for (size_t t = 0; t < T; ++t) {
                 uint32_t x = 0;
                 for (int h = 0; h < H; ++h)
@@ -163,38 +163,58 @@ std::vector<uint32_t> decode_n02(const BitF& bit, int len, int tb, double pd, Ct
     return x;
 }
 
-template <int N0>
-void decode_one(const uint8_t* w, int len, int n, double pd, Ctx& cx, std::vector<int>& xhat) {
+OnesProbs ones_probs(int ones, double pd) {  // as sc_del.hip's launcher
+    OnesProbs op;
+    op.ones = ones;
+    for (int i = 0; i < 4; ++i) op.pr[i] = 1.0;
+    double comb = 1.0;
+    for (int i = 0; ones > 0 && i <= ones; ++i) {
+        if (i > 0) comb = comb * (double)(ones - i + 1) / (double)i;
+        op.pr[i] = comb * std::pow(1.0 - pd, (double)i) * std::pow(pd, (double)(ones - i));
+    }
+    return op;
+}
+
+template <int N0, int OC>
+void decode_one_oc(const uint8_t* w, int len, int n, double pd, int ones, Ctx& cx, std::vector<int>& xhat) {
     constexpr int L = 1 << N0;
     const int tb = n - N0;
     const int T = 1 << tb;
     auto bit = [w](int i) { return (int)w[i]; };
-    std::vector<Trel<L, Cap<L>::V, Cap<L>::E0>> base(T);
+    const OnesProbs op = ones_probs(ones, pd);
+    std::vector<Trel<L, Cap<L, OC>::V, Cap<L, OC>::E0>> base(T);
     for (int t = 0; t < T; ++t) {
         int s, m;
         segment_of(bit, len, tb, t, s, m);
-        trellis_build<L>(base[t], bit, s, m, pd);
+        trellis_build<L>(base[t], bit, s, m, pd, op);
     }
     std::vector<uint32_t> x;
-    if constexpr (N0 == 2) {
+    if constexpr (N0 == 2 && OC == 0) {
         if (use_n02) {
             x = decode_n02(bit, len, tb, pd, cx);
         } else {
-            x = Node<L, L>::run(base, cx);
+            x = Node<L, L, OC>::run(base, cx, ones);
         }
     } else {
-        x = Node<L, L>::run(base, cx);
+        x = Node<L, L, OC>::run(base, cx, ones);
     }
     xhat.assign((size_t)T * L, 0);
     for (int t = 0; t < T; ++t)
         for (int i = 0; i < L; ++i) xhat[(size_t)t * L + i] = (int)((x[t] >> i) & 1u);
 }
 
+template <int N0>
+void decode_one(const uint8_t* w, int len, int n, double pd, int ones, Ctx& cx, std::vector<int>& xhat) {
+    if (ones > 0) decode_one_oc<N0, 3>(w, len, n, pd, ones, cx, xhat);
+    else decode_one_oc<N0, 0>(w, len, n, pd, ones, cx, xhat);
+}
+
 }  // namespace
 
 extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, long long B, int stride, int n, int n0,
-                                   double pd, const uint32_t* fmask, const uint32_t* fval, uint32_t* info,
+                                   int ones, double pd, const uint32_t* fmask, const uint32_t* fval, uint32_t* info,
                                    uint32_t* xhat) {
+    if (ones < 0 || ones > 3) return -1;
     const int N = 1 << n;
     int K = 0;
     for (int i = 0; i < N; ++i) K += 1 - fbit(fmask, i);
@@ -205,9 +225,10 @@ extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, lon
         const int len = rx_len[b];
         try {
             switch (n0) {
-                case 1: decode_one<1>(w, len, n, pd, cx, xh); break;
-                case 2: decode_one<2>(w, len, n, pd, cx, xh); break;
-                case 3: decode_one<3>(w, len, n, pd, cx, xh); break;
+                case 1: decode_one<1>(w, len, n, pd, ones, cx, xh); break;
+                case 2: decode_one<2>(w, len, n, pd, ones, cx, xh); break;
+                case 3: decode_one<3>(w, len, n, pd, ones, cx, xh); break;
+                case 4: decode_one<4>(w, len, n, pd, ones, cx, xh); break;
                 default: return -1;
             }
         } catch (int) {

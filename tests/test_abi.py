@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     H = ctypes.CDLL(build.HOST_LIB)  # host-only construction library (include/polarcub_construct.h)
     missing = [n for n in sorted(_declared("polarcub_construct.h")) if not hasattr(H, n)]
     assert not missing, missing
-    assert _lib.lib().pcub_abi_version() == 1
+    assert _lib.lib().pcub_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_invalid_arguments_are_rejected_without_touching_the_device():

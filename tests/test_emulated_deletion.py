@@ -23,7 +23,7 @@ def emu():
     return _L
 
 
-def run(rx, rx_len, n, n0, pd, frozen, fval):
+def run(rx, rx_len, n, n0, pd, frozen, fval, ones=0):
     B = rx.shape[0]
     N = 1 << n
     K = int(N - frozen.sum())
@@ -34,7 +34,7 @@ def run(rx, rx_len, n, n0, pd, frozen, fval):
     info = np.zeros((max(1, (K + 31) // 32), B), np.uint32)
     xh = np.zeros((max(1, (N + 31) // 32), B), np.uint32)
     P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-    rc = emu().emu_decode_deletion(P(rx), P(ln), ctypes.c_longlong(B), rx.shape[1], n, n0, ctypes.c_double(pd),
+    rc = emu().emu_decode_deletion(P(rx), P(ln), ctypes.c_longlong(B), rx.shape[1], n, n0, ones, ctypes.c_double(pd),
                                    P(fm), P(fv), P(info), P(xh))
     assert rc == 0
     return unpack_rows(info, K), unpack_rows(xh, N)
@@ -61,9 +61,9 @@ def test_c5_golden(n02):
 def test_edge_golden(idx, n02):
     c = deletion_edge_cases()[idx]
     n, n0, ones = (int(v) for v in c["shape"])
-    if ones != 0 or n0 > 3:
-        pytest.skip("outside the kernel's shapes (generic plugin path)")
-    info, xhat = run(c["rx"], c["rx_len"], n, n0, float(c["pd"][0]), c["frozen"], c["fval"])
+    if n02 and (n0 != 2 or ones != 0):
+        pytest.skip("the register-resident representation covers n0 = 2 without guard-band ones")
+    info, xhat = run(c["rx"], c["rx_len"], n, n0, float(c["pd"][0]), c["frozen"], c["fval"], ones)
     assert np.array_equal(info, c["info"])
     assert np.array_equal(xhat, c["xhat"])
 
@@ -105,3 +105,34 @@ def test_packed_segment_parse_matches_byte_parse():
     L = emu()
     L.emu_check_segments.restype = ctypes.c_longlong
     assert L.emu_check_segments(ctypes.c_uint64(12345), 3000) == 0
+
+
+@pytest.mark.parametrize("n0,n,ones", [(3, 10, 0), (3, 11, 0), (4, 12, 0), (4, 6, 0), (2, 5, 1), (1, 4, 2),
+                                       (3, 6, 3), (4, 6, 2), (2, 9, 0)])
+def test_wide_shapes_vs_oracle(n0, n, ones):
+    """Shapes the widened kernel adds: more than 64 trellises (main_deletion.py's n0 = n // 3
+    at n = 10..12), 16-input trellises and guard-band ones (capacities, vertex probabilities,
+    the materialised collapse), against the oracle."""
+    import random
+
+    from oracle import trellis_oracle as tro
+    N = 1 << n
+    rng = np.random.default_rng(97 * n + 7 * n0 + ones)
+    prng = random.Random(n + ones)
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    frozen[: N // 4] = 1
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    pd = [0.05, 0.1, 0.2][(n + ones) % 3]
+    words = []
+    for t in range(3 if n >= 10 else 8):
+        x = [int(b) for b in rng.integers(0, 2, N)]
+        words.append(tro.deletion_channel(tro.add_guard_bands(x, n, n0, 0.1, ones), pd, prng))
+    words += [[], [1, 1, 1], [int(b) for b in rng.integers(0, 2, N // 2)]]
+    W = max(len(w) for w in words)
+    rx = np.zeros((len(words), W), np.uint8)
+    for i, w in enumerate(words):
+        rx[i, :len(w)] = w
+    info, xhat = run(rx, np.array([len(w) for w in words], np.int32), n, n0, pd, frozen, fval, ones)
+    for i, w in enumerate(words):
+        xr, ir = tro.decode_deletion(w, n, n0, pd, frozen, fval, ones=ones)
+        assert list(info[i]) == ir and list(xhat[i]) == xr, i

@@ -22,9 +22,9 @@ def sc():
     return m
 
 
-def _dec(sc, n, n0, pd, frozen, fval, rx, rx_len):
+def _dec(sc, n, n0, pd, frozen, fval, rx, rx_len, ones=0):
     code = sc.CodeSpec(1 << n, frozen, fval, device="cuda")
-    d = sc.DeletionDecoder(code, n0, pd)
+    d = sc.DeletionDecoder(code, n0, pd, ones)
     info, xhat = d.decode(torch.from_numpy(np.ascontiguousarray(rx, np.uint8)).cuda(),
                           torch.from_numpy(np.asarray(rx_len, np.int32)).cuda())
     torch.cuda.synchronize()
@@ -43,41 +43,43 @@ def test_c5_golden(sc):
 def test_edge_golden(sc, idx):
     c = deletion_edge_cases()[idx]
     n, n0, ones = (int(v) for v in c["shape"])
-    if ones != 0 or not sc.deletion_supported(n, n0):
-        pytest.skip("outside the kernel's shapes (generic plugin path)")
-    info, xhat = _dec(sc, n, n0, float(c["pd"][0]), c["frozen"], c["fval"], c["rx"], c["rx_len"])
+    assert sc.deletion_supported(n, n0, ones)  # every golden shape (n0 = 4, guard-band ones) has a kernel
+    info, xhat = _dec(sc, n, n0, float(c["pd"][0]), c["frozen"], c["fval"], c["rx"], c["rx_len"], ones)
     assert np.array_equal(info, c["info"])
     assert np.array_equal(xhat, c["xhat"])
 
 
-SHAPES = [(n0, n0 + tb) for n0 in (1, 2, 3) for tb in range(1, 7)]
+SHAPES = ([(n0, n0 + tb, 0) for n0 in (1, 2, 3) for tb in range(1, 9)] + [(4, 4 + tb, 0) for tb in (1, 3, 5, 7, 8)]
+          + [(n0, n0 + tb, ones) for n0, tb, ones in ((1, 2, 1), (2, 3, 2), (3, 4, 3), (2, 7, 1), (4, 2, 2), (3, 8, 1))])
 
 
-@pytest.mark.parametrize("n0,n", SHAPES)
-def test_random_vs_oracle(sc, n0, n):
-    """Every kernel shape: channel outputs at several deletion rates plus adversarial words,
+@pytest.mark.parametrize("n0,n,ones", SHAPES)
+def test_random_vs_oracle(sc, n0, n, ones):
+    """Every kernel shape (2 .. 256 trellises of 2 .. 16 inputs, with and without
+    guard-band ones): channel outputs at several deletion rates plus adversarial words,
     random frozen sets (incl. all-frozen and all-information windows) vs the oracle."""
     N = 1 << n
-    rng = np.random.default_rng(1000 * n0 + n)
-    prng = random.Random(n)
+    rng = np.random.default_rng(1000 * n0 + 10 * n + ones)
+    prng = random.Random(n + 100 * ones)
     frozen = (rng.random(N) < 0.5).astype(np.uint8)
     frozen[: N // 4] = 1
     frozen[-(N // 8) or -1:] = 0
     fval = (rng.random(N) < 0.5).astype(np.uint8)
     pd = [0.05, 0.1, 0.3][n % 3]
     words = []
-    for t in range(10):
+    ntx = 10 if n <= 9 else 4
+    for t in range(ntx):
         x = [int(b) for b in rng.integers(0, 2, N)]
-        cw = tro.add_guard_bands(x, n, n0, 0.1)
-        words.append(tro.deletion_channel(cw, pd if t < 8 else 0.6, prng))
+        cw = tro.add_guard_bands(x, n, n0, 0.1, ones)
+        words.append(tro.deletion_channel(cw, pd if t < ntx - 2 else 0.6, prng))
     words += [[], [1], [0] * 9, [int(b) for b in rng.integers(0, 2, 3 * N)]]
     W = max(len(w) for w in words)
     rx = np.zeros((len(words), W), np.uint8)
     for i, w in enumerate(words):
         rx[i, :len(w)] = w
-    info, xhat = _dec(sc, n, n0, pd, frozen, fval, rx, [len(w) for w in words])
+    info, xhat = _dec(sc, n, n0, pd, frozen, fval, rx, [len(w) for w in words], ones)
     for i, w in enumerate(words):
-        x_ref, i_ref = tro.decode_deletion(w, n, n0, pd, frozen, fval)
+        x_ref, i_ref = tro.decode_deletion(w, n, n0, pd, frozen, fval, ones=ones)
         assert list(info[i]) == i_ref, (i, w)
         assert list(xhat[i]) == x_ref, (i, w)
 

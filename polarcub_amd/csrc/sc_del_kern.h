@@ -21,9 +21,9 @@
 // owns trellis bitrev(p)), decoded by the binary kernel's machinery:
 //   * T <= 32: across the codeword's lanes (XSub<T>, sc_bin_body.h);
 //   * T >= 64: the workgroup's 256 collapsed values go through LDS to wave 0, which
-//     decodes every codeword of the group at once with 64/CPB lanes per codeword and
-//     4 values per lane (WinTree<4, 64/CPB, T/64>: the binary kernel's register
-//     subtree, lane-local top levels + XSub), and hands back the encoding bits and
+//     decodes every codeword of the group at once with 16 lanes per codeword and T/16
+//     values per lane (WinTree<T/16, 16, T/64>: the binary kernel's register subtree,
+//     lane-local top levels + XSub<16>), and hands back the encoding bits and
 //     decisions through LDS.
 //
 // n0 = 2 without guard-band ones (main_deletion.py's default shape at n = 8) runs on
@@ -91,12 +91,60 @@ struct XSubE {
     }
 };
 
+// The wave-0 decode of a collapsed node of T > 64 rows (16 lanes per codeword, T/16
+// values per lane): WinTree's split at the top nodes, each 64-position window decoded by
+// one out-of-line copy of SubV<4, 0, 16> (the T = 64 decode).  Fully inlined, the node's
+// code passes the 16-bit branch range, and LLVM's long branches in a device function go
+// through the return-address registers s[30:31] (scripts/check_isa.py guards against it).
+struct V4 {
+    double v[4];
+};
+
+__device__ __attribute__((noinline)) uint32_t del_window(V4 x, uint64_t& ub, uint64_t fm, uint64_t fv, int lane) {
+    return SubV<4, 0, 16>::run(x.v, ub, fm, fv, lane);
+}
+
+template <int L, int NWIN>
+struct DelWin {
+    static __device__ __forceinline__ uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm,
+                                                   const uint64_t* fv, int lane) {
+        if constexpr (NWIN == 1) {
+            static_assert(L == 4, "one window = 4 values x 16 lanes");
+            V4 x;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) x.v[t] = v[t];
+            return del_window(x, ub[0], fm[0], fv[0], lane);
+        } else {
+            constexpr int H = L / 2;
+            constexpr int HW = NWIN / 2;
+            double c[H];
+            uint32_t ym, yp;
+            if (WinTree<L, 16, NWIN>::frozen_windows(fm)) {
+                ym = WinTree<H, 16, HW>::frozen(ub, fv, lane & 15);
+            } else {
+#pragma unroll
+                for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
+                ym = DelWin<H, HW>::run(c, ub, fm, fv, lane);
+            }
+            if (WinTree<L, 16, NWIN>::frozen_windows(fm + HW)) {
+                yp = WinTree<H, 16, HW>::frozen(ub + HW, fv + HW, lane & 15);
+            } else {
+#pragma unroll
+                for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
+                yp = DelWin<H, HW>::run(c, ub + HW, fm + HW, fv + HW, lane);
+            }
+            return (ym ^ yp) | (yp << H);
+        }
+    }
+};
+
 // Per-lane decoding context: frozen windows, decisions, information accumulator.
 template <int T, bool EXP>
 struct DelCtx {
     static constexpr int NW = T > 64 ? T / 64 : 1;  // 64-bit windows of a memoryless subtree
     static constexpr int CPB = kDelBlock / T;       // codewords per workgroup
-    static constexpr int GL = 64 / (CPB < 64 ? CPB : 64);  // wave-0 lanes per codeword (T >= 64)
+    static constexpr int GL = 16;                   // wave-0 lanes per codeword (T >= 64)
+    static constexpr int LV = T >= 64 ? T / GL : 1;  // values per wave-0 lane (T >= 64)
     DelArgs A;  // by value: taking the kernel argument's address would force it to scratch
     long long cw;
     bool leader;  // group position 0 stores the information words and exported leaves
@@ -107,7 +155,7 @@ struct DelCtx {
     int infow;
     // T >= 64, decode mode: exchange buffers in LDS (see subtree())
     double* xv;               // [256] collapsed values, codeword g's at [g*T, (g+1)*T)
-    unsigned long long* xb;   // [4] ballots of the encoding bits, one per local index
+    unsigned long long* xb;   // [LV] ballots of the encoding bits, one per local index
     unsigned long long* xub;  // [CPB][NW] decisions per codeword
 
     // bits [k*T + 64w, ...) of a bit vector whose word i is w[i * stride]
@@ -148,11 +196,12 @@ struct DelCtx {
             // One codeword per wave (or per workgroup) is the trellis stages' layout, but
             // a length-T subtree decoded across all those lanes spends a full wave op on
             // every node.  So the group's collapsed rows go through LDS to wave 0, which
-            // decodes them all at once with GL lanes per codeword, 4 values per lane (lane
-            // j of group c owns positions j + GL*t: the binary kernel's register subtree),
-            // and hands back the encoding bits and decisions.  fm / fv are the same for
-            // the whole group (per-codeword frozen values exist only in export mode), so
-            // every wave takes this branch together.
+            // decodes them all at once with GL = 16 lanes per codeword, LV = T/16 values
+            // per lane (lane j of group c owns positions j + 16t: the binary kernel's
+            // register subtree, WinTree<LV, 16, NW>), and hands back the encoding bits and
+            // decisions.  With CPB < 4 codewords the other lanes decode a copy and store
+            // nothing.  fm / fv are the same for the whole group (per-codeword frozen
+            // values exist only in export mode), so every wave takes this branch together.
             const int wv = threadIdx.x >> 6;
             xv[threadIdx.x] = v;
             __syncthreads();
@@ -160,19 +209,22 @@ struct DelCtx {
             // each, and beats rotating the decoding wave over the group's waves)
             if (wv == 0) {
                 const int c = lane / GL, j = lane % GL;
-                double vv[4];
+                const int cr = c < CPB ? c : CPB - 1;
+                double vv[LV];
 #pragma unroll
-                for (int t = 0; t < 4; ++t) vv[t] = xv[c * T + j + GL * t];
+                for (int t = 0; t < LV; ++t) vv[t] = xv[cr * T + j + GL * t];
                 uint64_t ubl[NW];
 #pragma unroll
                 for (int w = 0; w < NW; ++w) ubl[w] = 0;
-                const uint32_t bits = WinTree<4, GL, NW>::run(vv, ubl, fm, fv, lane);
+                uint32_t bits;
+                if constexpr (NW == 1) bits = WinTree<LV, GL, NW>::run(vv, ubl, fm, fv, lane);
+                else bits = DelWin<LV, NW>::run(vv, ubl, fm, fv, lane);
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
+                for (int t = 0; t < LV; ++t) {
                     const unsigned long long bal = __ballot((bits >> t) & 1u);
                     if (lane == 0) xb[t] = bal;
                 }
-                if (j == 0)
+                if (j == 0 && c < CPB)
 #pragma unroll
                     for (int w = 0; w < NW; ++w) xub[c * NW + w] = ubl[w];
             }
@@ -353,7 +405,8 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
     else segment_of(bit, len, TB, t, s, m);
 
     __shared__ double xv[(T >= 64 && !EXP) ? kDelBlock : 1];
-    __shared__ unsigned long long xb[4], xub[(T >= 64 && !EXP) ? CPB * DelCtx<T, EXP>::NW : 1];
+    __shared__ unsigned long long xb[(T >= 64 && !EXP) ? DelCtx<T, EXP>::LV : 1],
+        xub[(T >= 64 && !EXP) ? CPB * DelCtx<T, EXP>::NW : 1];
     DelCtx<T, EXP> cx;
     cx.xv = xv;
     cx.xb = xb;

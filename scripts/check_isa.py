@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""ISA hazard check of the built HIP library (gfx950 code object).
+
+LLVM's long-branch expansion (s_getpc_b64 / s_add / s_setpc_b64 through s[30:31]) inside
+a non-kernel device function clobbers the return address held in s[30:31]; the function
+then 'returns' into its own body.  Observed on a >128 KiB deletion-kernel callee (round 2),
+where it ended in an illegal memory access.  The library must not contain such a function:
+every device function must either be inlined or free of s_setpc_b64 s[30:31] other than
+its final return.
+
+    python scripts/check_isa.py [path/to/libpolarcub_hip.so]
+Exit status 1 lists the offending functions.
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def code_objects(lib):
+    """The gfx950 code objects of every translation unit: the library's .hip_fatbin section
+    is a sequence of clang offload bundles (magic, entry count, then offset/size/triple
+    per entry, offsets relative to the bundle)."""
+    import struct
+    with tempfile.TemporaryDirectory() as d:
+        fat = os.path.join(d, "fat.bin")
+        subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section", ".hip_fatbin=" + fat, lib,
+                        os.path.join(d, "stripped.so")], check=True)
+        data = open(fat, "rb").read()
+    out = []
+    pos = data.find(MAGIC)
+    while pos >= 0:
+        n = struct.unpack_from("<Q", data, pos + 24)[0]
+        q = pos + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", data, q)
+            triple = data[q + 24:q + 24 + tl].decode()
+            q += 24 + tl
+            if "gfx950" in triple and size:
+                out.append(data[pos + off:pos + off + size])
+        pos = data.find(MAGIC, pos + 24)
+    return out
+
+
+def device_disasm(lib):
+    texts = []
+    with tempfile.TemporaryDirectory() as d:
+        for i, co in enumerate(code_objects(lib)):
+            f = os.path.join(d, "co%d.o" % i)
+            with open(f, "wb") as fh:
+                fh.write(co)
+            texts.append(subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", f],
+                                        check=True, capture_output=True, text=True).stdout)
+    return "\n".join(texts)
+
+
+def main():
+    lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "polarcub_amd", "lib", "libpolarcub_hip.so")
+    text = device_disasm(lib)
+    bad = []
+    for m in re.finditer(r"^[0-9a-f]+ <([^>]+)>:\n(.*?)(?=^[0-9a-f]+ <|\Z)", text, re.S | re.M):
+        name, body = m.group(1), m.group(2)
+        if ".kd" in name:
+            continue
+        if "s_endpgm" in body:
+            continue
+        # a return is a bare s_setpc_b64 s[30:31] (tail duplication gives a function several);
+        # a long branch computes the target into the pair first (s_getpc_b64 + s_add/s_addc)
+        lines = body.splitlines()
+        n = 0
+        for i, line in enumerate(lines):
+            if "s_setpc_b64 s[30:31]" in line:
+                prev = " ".join(lines[max(0, i - 4):i])
+                if re.search(r"s_getpc_b64 s\[30:31\]|s_add_u32 s30|s_addc_u32 s31|s_sub_u32 s30", prev):
+                    n += 1
+        if n:
+            bad.append((name, n))
+    for name, n in bad:
+        print("long branch through the return address in device function %s (%d long branch(es) via s[30:31])" % (name, n))
+    print("%d function(s) checked, %d hazard(s)" % (len(re.findall(r"^[0-9a-f]+ <", text, re.M)), len(bad)))
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -54,3 +54,17 @@ def test_oracle_and_emulator_build():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "emu")], check=True)
     assert os.path.exists(os.path.join(ROOT, "oracle", "build", "liborc.so"))
     assert os.path.exists(os.path.join(ROOT, "tests", "emu", "build", "libemu.so"))
+
+
+def test_no_long_branch_through_the_return_address():
+    """scripts/check_isa.py: no device function of the built code object computes a long
+    branch into s[30:31] (LLVM's expansion clobbers the return address; seen as an illegal
+    memory access in a round-2 deletion callee)."""
+    import subprocess
+    import sys
+    from polarcub_amd import build
+    build.build()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_isa.py"), build.LIB],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 hazard(s)" in r.stdout

@@ -514,9 +514,17 @@ def main(argv=None):
     sync()
     log("rank %d: %s inputs for %d codewords generated in %.1f s" % (rank, a.workload, w.B, time.time() - t0))
 
-    for _ in range(a.warmup):
+    # a slow step (deletion at n >= 12) logs progress per step, so a long run is visibly alive;
+    # the per-step sync this adds is microseconds against tens of seconds
+    slow = False
+    for i in range(a.warmup):
+        tw = time.perf_counter()
         w.step()
-    sync()
+        sync()
+        dt = time.perf_counter() - tw
+        slow = slow or dt > 20.0
+        if slow:
+            log("rank %d: warmup step %d/%d %.1f s" % (rank, i + 1, a.warmup, dt))
     if world > 1:
         dist.barrier()
     sync()
@@ -532,6 +540,9 @@ def main(argv=None):
         w.step()
         if evs:
             evs[i][1].record(stream)
+        if slow:
+            sync()
+            log("rank %d: step %d/%d done at %.1f s" % (rank, i + 1, a.steps, time.perf_counter() - t_start))
     sync()
     t_local = time.perf_counter() - t_start  # this rank's own decode time
     if world > 1:

@@ -126,6 +126,24 @@ int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, i
                           int32_t ones, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
                           const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
                           double* leaf, void* stream);
+/* Non-uniform a-priori distribution (two trees).  Replaces recursiveEncodeDecode with an
+ * xVectorDistribution that is not uniform (BinaryPolarEncoderDecoder.py:223-325, called by
+ * decode :71-99 and encode :46-69): the prior tree px runs beside the xy tree through the same
+ * minus / plus / max-normalise steps; a frozen u_i = 0 iff the prior leaf's marginal
+ * m0 >= rnd[i] (:258-262), an information u_i is the xy leaf's decision (:249-252).
+ *   xy          [N][B][2] f64 joint pairs (decode), or NULL to encode: the information bits
+ *               are then READ from info_words and only the prior tree runs (:254)
+ *   px          [N][px_batch][2] f64 prior pairs, px_batch = 1 (one prior for the batch) or B
+ *   rnd         [N] f64 common randomness (randomlyGeneratedNumbers, :33-44)
+ *   leaf        NULL or [N][B] compact leaves of the deciding tree (xy; prior when encoding)
+ *               -- marginalizedUProbs (:267-273)
+ *   info_words  [ceil(K/32)][B]: written (decode) or read (encode); xhat_words may be NULL.
+ * log2N in 1..20; workspace of pcub_sc_prior_bin_workspace(B, log2N) bytes. */
+size_t pcub_sc_prior_bin_workspace(int64_t B, int32_t log2N);
+int pcub_sc_prior_bin(const double* xy, const double* px, int64_t px_batch, int64_t B, int32_t log2N,
+                      const uint32_t* frozen_mask, const double* rnd, int32_t K, uint32_t* info_words,
+                      uint32_t* xhat_words, double* leaf, void* workspace, size_t workspace_bytes, void* stream);
+
 /* compact leaves -> the reference's marginals (calcMarginalizedProbabilities,
  * VectorDistributions/BinaryMemorylessVectorDistribution.py:52-69): s = p0 + p1,
  * m = p / s, (0.5, 0.5) when s = 0.  count values in, [count][2] f64 out. */

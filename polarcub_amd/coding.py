@@ -20,9 +20,13 @@ HIP C ABI, bit-identical to the reference, for
   * a deletion-channel collection of trellises built from a received word by
     buildCollectionOfBinaryTrellises_uniformInput_deletion, in the shapes the
     deletion kernel covers (pcub_sc_decode_deletion).
-Any other plugin (other trellis shapes, user classes, non-uniform priors) goes
-through recursiveEncodeDecode, which drives the plugin's own methods exactly as
-the reference does.  Additions: decode_batch / encode_batch / decode_deletion_batch.
+Under a non-uniform memoryless binary prior, encode() and decode() of memoryless
+xy run the two-tree kernel (pcub_sc_prior_bin: prior and xy trees side by side,
+frozen bits drawn against the common randomness).  Any other plugin (other
+trellis shapes, user classes, non-memoryless priors) goes through
+recursiveEncodeDecode, which drives the plugin's own methods exactly as the
+reference does.  Additions: decode_batch / encode_batch / decode_deletion_batch /
+decode_prior_batch / encode_prior_batch.
 """
 import random
 import sys
@@ -48,6 +52,17 @@ def _is_uniform_prior(xvd):
         return False
     p = np.asarray(xvd.probs, dtype=np.float64)
     return p.ndim == 2 and p.shape[1] == 2 and bool(np.all(p[:, 0] == p[:, 1])) and bool(np.all(np.isfinite(p)))
+
+
+def _prior_rows(xvd, length):
+    """The prior rows [N, 2] when xvd is a memoryless binary prior the two-tree kernel takes
+    (finite, non-negative; N >= 2), else None."""
+    if length < 2 or not _is_memoryless_binary(xvd):
+        return None
+    p = np.asarray(xvd.probs, dtype=np.float64)
+    if p.shape != (length, 2) or not np.all(np.isfinite(p)) or not np.all(p >= 0):
+        return None
+    return p
 
 
 def _deletion_kernel_shape(xyvd, leaves=False):
@@ -118,7 +133,37 @@ class BinaryPolarEncoderDecoder:
             self._device_key = key
         return self._device_code
 
+    def _prior(self):
+        from . import sc
+        code = self._code()
+        if getattr(self, "_prior_key", None) != self._device_key:
+            self._prior_coder = sc.PriorCoder(code, self.randomlyGeneratedNumbers)
+            self._prior_key = self._device_key
+        return self._prior_coder
+
     # -- batched device entry points -------------------------------------------
+    def decode_prior_batch(self, prior, xy):
+        """Two-tree decode under a non-uniform prior: prior [N, 2] (or [B, N, 2] per codeword),
+        xy [B, N, 2].  Returns (encodedVectors int64[B, N], information int64[B, k])."""
+        import torch
+        pc = self._prior()
+        dev = pc.code.device
+        px = torch.as_tensor(np.asarray(prior, dtype=np.float64), device=dev)
+        if px.dim() == 3:
+            px = px.transpose(0, 1)
+        info, xh = pc.decode(px, torch.as_tensor(np.asarray(xy, dtype=np.float64), device=dev))
+        return xh.cpu().numpy().astype(np.int64), info.cpu().numpy().astype(np.int64)
+
+    def encode_prior_batch(self, prior, information):
+        """Encode [B, k] information bits under a non-uniform prior [N, 2]; frozen bits follow
+        the prior tree and the common randomness (BinaryPolarEncoderDecoder.py:46-69, 258-262)."""
+        import torch
+        pc = self._prior()
+        dev = pc.code.device
+        inf = torch.as_tensor(np.asarray(information, dtype=np.uint8).reshape(-1, self.k), device=dev)
+        return pc.encode(torch.as_tensor(np.asarray(prior, dtype=np.float64), device=dev), inf).cpu().numpy().astype(
+            np.int64)
+
     def decode_batch(self, xy):
         """xy: [B, N, 2] joint probabilities (numpy or torch), uniform prior.
         Returns (encodedVectors int64[B, N], information int64[B, k]) as numpy arrays."""
@@ -161,6 +206,9 @@ class BinaryPolarEncoderDecoder:
         assert len(information) == self.k
         if _is_uniform_prior(xVectorDistribution):
             return self.encode_batch(np.asarray(information, dtype=np.uint8)[None, :])[0]
+        prior = _prior_rows(xVectorDistribution, self.length)
+        if prior is not None:
+            return self.encode_prior_batch(prior, np.asarray(information, dtype=np.uint8)[None, :])[0]
         (enc, nu, ni) = self.recursiveEncodeDecode(information, 0, 0, self.randomlyGeneratedNumbers,
                                                    xVectorDistribution)
         assert nu == len(enc) == len(xVectorDistribution)
@@ -177,6 +225,10 @@ class BinaryPolarEncoderDecoder:
         if shape is not None and _is_uniform_prior(xVectorDistribution):
             enc, info = self.decode_deletion_batch([xyVectorDistribution.deletion_source[0]], shape[0], shape[2],
                                                    shape[3])
+            return (enc[0], info[0])
+        prior = _prior_rows(xVectorDistribution, self.length)
+        if prior is not None and _is_memoryless_binary(xyVectorDistribution):
+            enc, info = self.decode_prior_batch(prior, _check_joint(xyVectorDistribution.probs)[None, :, :])
             return (enc[0], info[0])
         information = np.empty(self.k, np.int64)
         information[:] = -1
@@ -297,12 +349,15 @@ def encodeDecodeSimulation(length, make_xVectorDistribution, make_codeword, simu
     errors = 0
     chunk = 1 << 16
     uniform = _is_uniform_prior(xvd)
+    prior = None if uniform else _prior_rows(xvd, length)
     for t0 in range(0, numberOfTrials, chunk):
         T = min(chunk, numberOfTrials - t0)
         infos = np.array([[0 if rng.random() < 0.5 else 1 for _ in range(encDec.k)] for _ in range(T)],
                          dtype=np.int64).reshape(T, encDec.k)
         if uniform:
             encoded = encDec.encode_batch(infos)
+        elif prior is not None:
+            encoded = encDec.encode_prior_batch(prior, infos)
         else:
             encoded = np.stack([encDec.encode(xvd, list(infos[t])) for t in range(T)])
         batch_xy, batch_del, pending = [], {}, []
@@ -311,7 +366,7 @@ def encodeDecodeSimulation(length, make_xVectorDistribution, make_codeword, simu
             received = simulateChannel(codeword)
             xyvd = make_xyVectrorDistribution(received)
             shape = _deletion_kernel_shape(xyvd) if uniform else None
-            if uniform and _is_memoryless_binary(xyvd):
+            if (uniform or prior is not None) and _is_memoryless_binary(xyvd):
                 pending.append((t, codeword, received, ("bin", len(batch_xy))))
                 batch_xy.append(_check_joint(xyvd.probs))
             elif shape is not None:
@@ -321,8 +376,10 @@ def encodeDecodeSimulation(length, make_xVectorDistribution, make_codeword, simu
             else:
                 pending.append((t, codeword, received, encDec.decode(xvd, xyvd)[1]))
         results = {}
-        if batch_xy:
+        if batch_xy and uniform:
             results["bin"] = encDec.decode_batch(np.stack(batch_xy))[1]
+        elif batch_xy:
+            results["bin"] = encDec.decode_prior_batch(prior, np.stack(batch_xy))[1]
         for shape, words in batch_del.items():
             results[shape] = encDec.decode_deletion_batch(words, shape[0], shape[2], shape[3])[1]
         for (t, codeword, received, info_t) in pending:

@@ -234,6 +234,75 @@ class LeafDecoder:
         return unpack(info, self.code.K), unpack(xh, self.code.N), leaf_marginals(leaf)
 
 
+class PriorCoder:
+    """Two-tree SC for a non-uniform a-priori distribution (pcub_sc_prior_bin): decode with
+    (prior, xy) or encode with the prior alone, frozen bits drawn against the common randomness
+    r_i (BinaryPolarEncoderDecoder.py:223-325, :258-262).  The code's frozen values are not
+    used: they follow from the prior tree."""
+
+    def __init__(self, code, rnd):
+        self.code = code
+        r = np.asarray(rnd, dtype=np.float64).reshape(-1)
+        if r.shape[0] != code.N:
+            raise ValueError("common randomness has %d entries, expected N=%d" % (r.shape[0], code.N))
+        self.rnd_dev = torch.from_numpy(r.copy()).to(code.device)
+        self._ws = None
+
+    def _prior(self, px, B):
+        c = self.code
+        px = torch.as_tensor(px, dtype=torch.float64, device=c.device)
+        if px.dim() == 2:  # [N, 2]: one prior for the whole batch
+            px = px[:, None, :]
+        if px.dim() != 3 or px.shape[0] != c.N or px.shape[2] != 2 or px.shape[1] not in (1, B):
+            raise ValueError("prior must be float64 [N, 2], [N, 1, 2] or [N, B, 2] with N=%d" % c.N)
+        return px.contiguous()
+
+    def run_native(self, px, xy=None, info_words=None, B=None, want_leaf=False):
+        """Decode (xy [N, B, 2] given) or encode (info_words [ceil(K/32), B] given).
+        Returns (info_words, xhat_words, leaf [N, B] compact | None)."""
+        c = self.code
+        if c.n < 1:
+            raise ValueError("two-tree SC needs N >= 2")
+        if xy is not None:
+            if xy.dtype != torch.float64 or xy.dim() != 3 or xy.shape[0] != c.N or xy.shape[2] != 2 or not xy.is_cuda:
+                raise ValueError("xy must be a float64 [N, B, 2] device tensor with N=%d" % c.N)
+            xy = xy.contiguous()
+            B = xy.shape[1]
+        else:
+            B = info_words.shape[1] if info_words is not None else int(B)
+        px = self._prior(px, B)
+        dev = c.device
+        need = int(_lib.lib().pcub_sc_prior_bin_workspace(B, c.n))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 16), dtype=torch.uint8, device=dev)
+        if xy is not None:
+            info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=dev)
+        else:
+            info = info_words.contiguous() if info_words is not None else torch.zeros((1, B), dtype=torch.int32,
+                                                                                      device=dev)
+        xh = torch.empty((c.n_words, B), dtype=torch.int32, device=dev)
+        leaf = torch.empty((c.N, B), dtype=torch.float64, device=dev) if want_leaf else None
+        rc = _lib.lib().pcub_sc_prior_bin(_p(xy), _p(px), px.shape[1], B, c.n, _p(c.fmask_dev), _p(self.rnd_dev), c.K,
+                                          _p(info), _p(xh), _p(leaf), _p(self._ws), self._ws.numel(), _stream())
+        _lib.check(rc, "pcub_sc_prior_bin")
+        return info, xh, leaf
+
+    def decode(self, px, xy, want_marginals=False):
+        """xy [B, N, 2] per-codeword rows -> (info [B, K] uint8, xhat [B, N] uint8[, marginals [B, N, 2]])."""
+        info, xh, leaf = self.run_native(px, xy=transpose_pairs(xy), want_leaf=want_marginals)
+        out = (unpack(info, self.code.K), unpack(xh, self.code.N))
+        return out + (leaf_marginals(leaf),) if want_marginals else out
+
+    def encode(self, px, info):
+        """info [B, K] uint8 -> codewords [B, N] uint8 under the prior."""
+        c = self.code
+        if info.shape[1] != c.K:
+            raise ValueError("info has %d columns, code has K=%d" % (info.shape[1], c.K))
+        words = pack(info) if c.K > 0 else None
+        _, xh, _ = self.run_native(px, info_words=words, B=info.shape[0])
+        return unpack(xh, c.N)
+
+
 def leaf_marginals(leaf):
     """Compact leaves [N, B] -> the reference's leaf marginals [B, N, 2] (pcub_leaf_marginals)."""
     N, B = leaf.shape

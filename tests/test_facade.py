@@ -31,17 +31,26 @@ def test_generic_recursion_matches_reference_uniform():
         assert np.array_equal(x, g["xhat"][b])
 
 
-def test_nonuniform_prior_goes_through_plugin_recursion():
+def test_nonuniform_prior_plugin_recursion():
+    """The generic recursion (the path of non-memoryless priors) on the two-tree golden set."""
     g = load_golden("prior_n64")
     fs = set(int(i) for i in np.nonzero(g["frozen"])[0])
     enc = coding.BinaryPolarEncoderDecoder(64, fs, 11)
     xvd = _bmvd(np.tile(g["prior"], (64, 1)))
     for b in range(0, g["xy"].shape[0], 3):
-        x, info = enc.decode(xvd, _bmvd(g["xy"][b]))
+        info = np.full(enc.k, -1, np.int64)
+        x, nu, ni = enc.recursiveEncodeDecode(info, 0, 0, enc.randomlyGeneratedNumbers, xvd, _bmvd(g["xy"][b]))
         assert np.array_equal(info, g["info"][b])
         assert np.array_equal(x, g["xhat"][b])
     for b in range(g["enc_info"].shape[0]):
-        assert np.array_equal(enc.encode(xvd, list(g["enc_info"][b])), g["enc_x"][b])
+        x, nu, ni = enc.recursiveEncodeDecode(list(g["enc_info"][b]), 0, 0, enc.randomlyGeneratedNumbers, xvd)
+        assert np.array_equal(x, g["enc_x"][b])
+
+
+def test_prior_rows_dispatch_rule():
+    assert coding._prior_rows(_bmvd(np.tile([0.7, 0.3], (8, 1))), 8) is not None
+    assert coding._prior_rows(_bmvd(np.tile([0.7, 0.3], (1, 1))), 1) is None  # N = 1: recursion
+    assert coding._prior_rows(_bmvd(np.tile([np.nan, 0.3], (8, 1))), 8) is None
 
 
 def test_polar_transform_of_bits():

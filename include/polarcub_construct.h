@@ -9,6 +9,7 @@
  *   pcub_bmd_degrade           BinaryMemorylessDistribution.degrade(L), after the merge  :287-346
  *   pcub_bmd_upgrade           BinaryMemorylessDistribution.upgrade(L), after the merge  :348-427
  *   pcub_bin_construct         calcFrozenSet_degradingUpgrading's TV / Pe vectors        :624-680
+ *   pcub_qmd_* / pcub_qary_construct  the q-ary construction (below)
  * Letters are [n][2] doubles (p(y, x=0), p(y, x=1)), the reference's probs rows.
  * Results are bit-identical to the reference (tests/test_construct.py).
  *
@@ -51,6 +52,25 @@ int pcub_bmd_upgrade(const double* merged, int64_t n, int64_t L, double* out, in
  * xprobs is NULL), leaves in u order; `threads` workers (< 1: all cores). */
 int pcub_bin_construct(int32_t n, int64_t L, const double* xprobs, int64_t nx, const double* xyprobs, int64_t nxy,
                        double* TV, double* Pe, int32_t threads);
+
+/* q-ary (ScalarDistributions/QaryMemorylessDistribution.py).  Distributions are [n][q] doubles
+ * (probs[y][x]), 2 <= q <= 64.
+ *   pcub_qmd_degrade     degrade(L) = degrade_dynamic :218-260 (one-hot binary channels degraded
+ *                        to M = floor(L^(1/(q-1))) letters each, product re-indexing, zero rows
+ *                        removed, normalised)
+ *   pcub_qmd_upgrade     upgrade(L) = upgrade_dynamic :329-475
+ *   pcub_qmd_error_prob  errorProb :53-61 and totalVariation :87-96
+ *   pcub_qary_construct  calcTVAndPe_degradingUpgrading's TV / Pe vectors :934-991 (x tree
+ *                        upgraded, xy tree degraded; TV = 0 when xprobs is NULL)
+ * out holds out_cap rows; *out_n receives the row count (PCUB_EINVAL when it exceeds out_cap;
+ * at most M^(q-1) <= L rows). */
+int pcub_qmd_degrade(int32_t q, const double* probs, int64_t n, int64_t L, double* out, int64_t out_cap,
+                     int64_t* out_n);
+int pcub_qmd_upgrade(int32_t q, const double* probs, int64_t n, int64_t L, double* out, int64_t out_cap,
+                     int64_t* out_n);
+int pcub_qmd_error_prob(int32_t q, const double* probs, int64_t n, double* pe, double* tv);
+int pcub_qary_construct(int32_t q, int32_t n, int64_t L, const double* xprobs, int64_t nx, const double* xyprobs,
+                        int64_t nxy, double* TV, double* Pe, int32_t threads);
 
 #ifdef __cplusplus
 }

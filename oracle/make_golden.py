@@ -927,6 +927,110 @@ def fx_qary_harness(R, timing):
     save("qary_harness", dict(runs=runs), **out)
 
 
+def _joint(QMD, prior, W):
+    """Joint q-ary distribution probs[y][x] = prior[x] * W[x][y] (build-side choice)."""
+    q = len(prior)
+    d = QMD.QaryMemorylessDistribution(q)
+    for y in range(len(W[0])):
+        d.append([prior[x] * W[x][y] for x in range(q)])
+    return d
+
+
+def fx_construct_qary_up(R, timing):
+    """q-ary upgrading (QaryMemorylessDistribution.upgrade_dynamic, :329-475: one-hot binary
+    channels upgraded with left/centre/right auxiliary sets, then recombined letter by letter)
+    on a-priori distributions (makeInputDistribution) and joint channels and their polar
+    transforms, and whole trees with an a-priori distribution (TV from the upgraded x tree,
+    calcTVAndPe_degradingUpgrading :934-991) and their frozen sets."""
+    import copy
+    QMD, QPED = R["QMD"], R["QPED"]
+    arrays, cases, trees, errors = {}, [], [], {}
+    W3 = [[0.7, 0.2, 0.1], [0.15, 0.7, 0.15], [0.1, 0.2, 0.7]]
+    srcs = {"x3": QMD.makeInputDistribution([0.5, 0.3, 0.2]), "x4": QMD.makeInputDistribution([0.4, 0.3, 0.2, 0.1]),
+            "x5": QMD.makeInputDistribution([0.3, 0.25, 0.2, 0.15, 0.1]),
+            "j3": _joint(QMD, [0.5, 0.3, 0.2], W3), "qsc4": QMD.makeQSC(4, 0.11), "qec3": QMD.makeQEC(3, 0.3)}
+    for cname, ch in srcs.items():
+        variants = {"": ch, "m": ch.minusTransform(), "p": ch.plusTransform()}
+        if ch.q <= 4:
+            variants["mp"] = variants["m"].plusTransform()
+            variants["pm"] = variants["p"].minusTransform()
+        for vname, d0 in variants.items():
+            case = cname + ("_" + vname if vname else "")
+            arrays[case + "_in"] = np.array(d0.probs, np.float64)
+            for L in (4, 9, 16, 64):
+                for op in ("up", "deg"):
+                    try:
+                        o = getattr(copy.deepcopy(d0), "upgrade" if op == "up" else "degrade")(L)
+                        arrays["%s_%s%d" % (case, op, L)] = np.array(o.probs, np.float64).reshape(-1, ch.q)
+                    except Exception as e:  # the reference's own failure, recorded as the expected outcome
+                        errors["%s_%s%d" % (case, op, L)] = type(e).__name__
+            cases.append(case)
+    for tname, q, n, L, prior, kinfo in (("j3_n4_L16", 3, 4, 16, [0.5, 0.3, 0.2], 5),
+                                         ("j3_n5_L9", 3, 5, 9, [0.5, 0.3, 0.2], 10),
+                                         ("j4_n3_L27", 4, 3, 27, [0.4, 0.3, 0.2, 0.1], 3)):
+        t0 = time.time()
+        if q == 3:
+            xy = _joint(QMD, prior, W3)
+        else:
+            W4 = [[0.85 if x == y else 0.05 for y in range(4)] for x in range(4)]
+            xy = _joint(QMD, prior, W4)
+        xd = QMD.makeInputDistribution(prior)
+        tv, pe = _qary_tv_pe(R, n, L, xy, xd)
+        bound = 0.2
+        fz = QPED.frozenSetFromTVAndPe(tv, pe, None if kinfo is not None else bound, kinfo)
+        mask = np.zeros(1 << n, np.uint8)
+        mask[sorted(fz)] = 1
+        arrays[tname + "_xy"] = np.array(xy.probs, np.float64)
+        arrays[tname + "_x"] = np.array(xd.probs, np.float64)
+        arrays[tname + "_tv"] = tv
+        arrays[tname + "_pe"] = pe
+        arrays[tname + "_frozen"] = mask
+        trees.append({"name": tname, "q": q, "n": n, "L": L, "prior": prior, "numInfoIndices": kinfo,
+                      "bound": None if kinfo is not None else bound, "K": int((1 << n) - mask.sum()),
+                      "seconds": round(time.time() - t0, 1)})
+        print("  tree %s: K=%d (%.1f s)" % (tname, (1 << n) - mask.sum(), time.time() - t0))
+    save("construct_qary_up", {"cases": cases, "trees": trees, "errors": errors,
+                               "note": "reference QaryMemorylessDistribution.upgrade/degrade and "
+                                       "calcTVAndPe_degradingUpgrading with an a-priori distribution"}, **arrays)
+
+
+def fx_combine_codes(R, timing):
+    """The reference's combine_codes.py itself (runpy, its own argv) on two frozen-set files in
+    BinaryPolarEncoderDecoder's genie format (build-side synthetic contents): printed line and
+    the 'out' file it writes."""
+    import contextlib
+    import io
+    import runpy
+    import tempfile
+    rng = np.random.default_rng(77)
+    files, texts = [], []
+    with tempfile.TemporaryDirectory() as d:
+        for k, (N, M) in enumerate(((64, 100), (64, 250))):
+            v = rng.random(N) * rng.choice([0.0, 1.0, 30.0], N)
+            lines = ["* main_deletion.py -n 6 -g %d" % M]
+            lines += [str(i) for i in range(0, N, 3)]
+            lines += ["** number of trials = %d" % M, "* (TotalVariation+errorProbability) * (number of trials)"]
+            lines += ["*** %d %s" % (i, repr(float(v[i]))) for i in range(N)]
+            path = os.path.join(d, "frozen%d.txt" % k)
+            with open(path, "w") as f:
+                f.write("\n".join(lines) + "\n")
+            files.append(path)
+            texts.append("\n".join(lines) + "\n")
+        cwd, argv = os.getcwd(), sys.argv
+        buf = io.StringIO()
+        try:
+            os.chdir(d)
+            sys.argv = ["combine_codes.py"] + files
+            with contextlib.redirect_stdout(buf):
+                runpy.run_path(os.path.join(REF, "combine_codes.py"), run_name="__main__")
+        finally:
+            os.chdir(cwd)
+            sys.argv = argv
+        out = open(os.path.join(d, "out")).read()
+    save("combine_codes", {"argv_files": 2}, inputs=np.array(texts), stdout=np.array(buf.getvalue()),
+         out=np.array(out))
+
+
 def fx_qary_log(R, timing):
     """use_log=True q-ary decodes (VectorDistributions/QaryMemorylessVectorDistribution.py:40,92-118:
     logaddexp transforms, logsumexp normalisation, log-domain marginals): QSC received words and
@@ -1013,6 +1117,8 @@ FIXTURES = {
     "construct_qary": fx_construct_qary,
     "qary_harness": fx_qary_harness,
     "qary_log": fx_qary_log,
+    "construct_qary_up": fx_construct_qary_up,
+    "combine_codes": fx_combine_codes,
 }
 
 

@@ -33,7 +33,7 @@ CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-fno-fast-math"
 
 
 HOST_LIB = os.path.join(LIBDIR, "libpolarcub_construct.so")
-HOST_SOURCES = [os.path.join(CSRC, "host", "tv_construct.cpp")]
+HOST_SOURCES = [os.path.join(CSRC, "host", "tv_construct.cpp"), os.path.join(CSRC, "host", "qary_construct.cpp")]
 CXX = os.environ.get("CXX", "g++")
 HOST_CFLAGS = ["-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-std=c++17", "-Wall", "-pthread"]
 
@@ -70,7 +70,8 @@ def _write_stamp(target, digest):
 
 def build_host(force=False, verbose=False):
     """The construction library: plain C++, IEEE binary64 without contraction, libm log2."""
-    deps = HOST_SOURCES + [os.path.join(ROOT, "include", "polarcub_construct.h")]
+    deps = HOST_SOURCES + [os.path.join(ROOT, "include", "polarcub_construct.h"),
+                           os.path.join(CSRC, "host", "tv_core.h")]
     dig = _digest(deps, [CXX] + HOST_CFLAGS)
     if not force and not _stale(HOST_LIB, dig):
         return HOST_LIB

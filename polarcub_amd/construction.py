@@ -7,6 +7,10 @@
   include/polarcub_construct.h), bit-identical to the reference, with the 2^m
   channels of each tree level on a thread pool: merge_equivalent / degrade /
   upgrade / tv_pe here, calcFrozenSet_degradingUpgrading in polarcub_amd.scalar.
+* The q-ary degrading/upgrading construction (ScalarDistributions/QaryMemorylessDistribution.py:
+  98-153, 218-260, 329-475, 934-991) in the same library (csrc/host/qary_construct.cpp):
+  qmd_degrade / qmd_upgrade / qary_tv_pe here; the reference-named classes and
+  calcFrozenSet_degradingUpgrading with its .npy cache in polarcub_amd.scalar_qary.
 * bhattacharyya_frozen: the standard Bhattacharyya-parameter recursion for BI-AWGN
   in the reference's index convention (minus child = first half of the u range,
   BinaryPolarEncoderDecoder.py:289-317), used for the benchmark's code.
@@ -14,6 +18,7 @@
 import ctypes
 import math
 import os
+import sys
 
 import numpy as np
 
@@ -36,7 +41,12 @@ def host_lib():
         lib.pcub_bmd_degrade.argtypes = [P, I64, I64, P, P, P]
         lib.pcub_bmd_upgrade.argtypes = [P, I64, I64, P, P]
         lib.pcub_bin_construct.argtypes = [I32, I64, P, I64, P, I64, P, P, I32]
-        for f in (lib.pcub_bmd_merge_equivalent, lib.pcub_bmd_degrade, lib.pcub_bmd_upgrade, lib.pcub_bin_construct):
+        lib.pcub_qmd_degrade.argtypes = [I32, P, I64, I64, P, I64, P]
+        lib.pcub_qmd_upgrade.argtypes = [I32, P, I64, I64, P, I64, P]
+        lib.pcub_qmd_error_prob.argtypes = [I32, P, I64, P, P]
+        lib.pcub_qary_construct.argtypes = [I32, I32, I64, P, I64, P, I64, P, P, I32]
+        for f in (lib.pcub_bmd_merge_equivalent, lib.pcub_bmd_degrade, lib.pcub_bmd_upgrade, lib.pcub_bin_construct,
+                  lib.pcub_qmd_degrade, lib.pcub_qmd_upgrade, lib.pcub_qmd_error_prob, lib.pcub_qary_construct):
             f.restype = ctypes.c_int
         _HOST = lib
     return _HOST
@@ -97,6 +107,56 @@ def tv_pe(n, L, xprobs, xyprobs, threads=0):
     Pe = np.empty(N)
     _check(host_lib().pcub_bin_construct(int(n), int(L), _ptr(x), 0 if x is None else len(x), _ptr(xy), len(xy),
                                          _ptr(TV), _ptr(Pe), int(threads)), "calcFrozenSet_degradingUpgrading")
+    return TV, Pe
+
+
+def _qrows(q, probs):
+    a = np.ascontiguousarray(np.asarray(probs, dtype=np.float64).reshape(-1, int(q)))
+    return a
+
+
+def calc_m(q, L):
+    """calcMFromL (ScalarDistributions/QaryMemorylessDistribution.py:753-755)."""
+    return math.floor(L ** (1.0 / (q - 1)) + sys.float_info.epsilon)
+
+
+def _qmd(fn, what, q, probs, L):
+    a = _qrows(q, probs)
+    cap = max(1, calc_m(q, L)) ** (q - 1)
+    out = np.empty((cap, q))
+    n = ctypes.c_int64(0)
+    _check(fn(int(q), _ptr(a), len(a), int(L), _ptr(out), cap, ctypes.byref(n)), what)
+    return out[:n.value].copy()
+
+
+def qmd_degrade(q, probs, L):
+    """QaryMemorylessDistribution.degrade(L) (degrade_dynamic, :218-260) of rows [n][q]."""
+    return _qmd(host_lib().pcub_qmd_degrade, "degrade", q, probs, L)
+
+
+def qmd_upgrade(q, probs, L):
+    """QaryMemorylessDistribution.upgrade(L) (upgrade_dynamic, :329-475) of rows [n][q]."""
+    return _qmd(host_lib().pcub_qmd_upgrade, "upgrade", q, probs, L)
+
+
+def qmd_error_prob_tv(q, probs):
+    """(errorProb, totalVariation) of rows [n][q] (:53-61, :87-96)."""
+    a = _qrows(q, probs)
+    pe, tv = ctypes.c_double(0.0), ctypes.c_double(0.0)
+    _check(host_lib().pcub_qmd_error_prob(int(q), _ptr(a), len(a), ctypes.byref(pe), ctypes.byref(tv)), "errorProb")
+    return pe.value, tv.value
+
+
+def qary_tv_pe(q, n, L, xprobs, xyprobs, threads=0):
+    """(TV, Pe) of calcTVAndPe_degradingUpgrading (:934-991): Pe of the degraded xy tree, TV of
+    the upgraded x tree (zeros when xprobs is None), leaves in u order."""
+    xy = _qrows(q, xyprobs)
+    x = None if xprobs is None else _qrows(q, xprobs)
+    N = 1 << n
+    TV = np.empty(N)
+    Pe = np.empty(N)
+    _check(host_lib().pcub_qary_construct(int(q), int(n), int(L), _ptr(x), 0 if x is None else len(x), _ptr(xy),
+                                          len(xy), _ptr(TV), _ptr(Pe), int(threads)), "calcTVAndPe_degradingUpgrading")
     return TV, Pe
 
 

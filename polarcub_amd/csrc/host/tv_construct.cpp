@@ -18,6 +18,7 @@
 //   LinkedListHeap (array min-heap over a doubly linked list, the reference's
 //   tie behaviour: an element rises past an equal key)  ScalarDistributions/UpgradingDegrading/LinkedListHeap.py:4-191
 // The construction runs the 2^m independent channels of each level on a thread pool.
+// The binary core (tv_core.h) is shared with the q-ary construction (qary_construct.cpp).
 #include <math.h>
 #include <stdint.h>
 
@@ -27,20 +28,10 @@
 #include <vector>
 
 #include "polarcub_construct.h"
+#include "tv_core.h"
 
-namespace {
-
-struct Letter {
-    double p0, p1;
-};
-
-// Failures the reference reports as Python exceptions.
-struct Err {
-    int code = 0;
-    void set(int c) {
-        if (!code) code = c;
-    }
-};
+namespace pcub {
+namespace tv {
 
 const double kInf = INFINITY;
 
@@ -343,9 +334,17 @@ double key_upgrade(const Letter& l, const Letter& c, const Letter& r, Err& err) 
     return hxgiveny(c, err) - hxgiveny(ml, err) - hxgiveny(mr, err);
 }
 
-std::vector<Letter> upgrade_merged(const std::vector<Letter>& in, int64_t L, Err& err) {
+std::vector<Letter> upgrade_merged(const std::vector<Letter>& in, int64_t L, Err& err, std::vector<UpAux>* aux) {
     const int64_t n = (int64_t)in.size();
     std::vector<Letter> d = in;
+    // auxiliary [left, centre, right] member lists per element (:368-401): a removed centre's
+    // centre and right members join its left neighbour's right set, its centre and left
+    // members its right neighbour's left set
+    std::vector<UpAux> ax;
+    if (aux) {
+        ax.resize(n);
+        for (int64_t i = 0; i < n; ++i) ax[i].c.push_back(i);
+    }
     std::vector<double> keys(n);
     for (int64_t i = 0; i < n; ++i)
         keys[i] = (i == 0 || i == n - 1) ? kInf : key_upgrade(d[i - 1], d[i], d[i + 1], err);
@@ -363,11 +362,25 @@ std::vector<Letter> upgrade_merged(const std::vector<Letter>& in, int64_t L, Err
         d[r].p0 += mr.p0;
         d[l].p1 += ml.p1;
         d[r].p1 += mr.p1;
+        if (aux) {
+            UpAux& A = ax[t];
+            std::vector<int64_t>& lr = ax[l].r;
+            lr.insert(lr.end(), A.c.begin(), A.c.end());
+            lr.insert(lr.end(), A.r.begin(), A.r.end());
+            std::vector<int64_t>& rl = ax[r].l;
+            rl.insert(rl.end(), A.c.begin(), A.c.end());
+            rl.insert(rl.end(), A.l.begin(), A.l.end());
+            A = UpAux();
+        }
         if (h.prev[l] >= 0) h.update(l, key_upgrade(d[h.prev[l]], d[l], d[r], err));
         if (h.next[r] >= 0) h.update(r, key_upgrade(d[l], d[r], d[h.next[r]], err));
     }
     std::vector<Letter> out;
-    for (int64_t e = h.head(); e >= 0; e = h.next[e]) out.push_back(d[e]);
+    if (aux) aux->clear();
+    for (int64_t e = h.head(); e >= 0; e = h.next[e]) {
+        out.push_back(d[e]);
+        if (aux) aux->push_back(std::move(ax[e]));
+    }
     return out;
 }
 
@@ -395,7 +408,7 @@ std::vector<Letter> child(const std::vector<Letter>& p, bool plus, bool up, int6
     std::vector<Letter> t = plus ? plus_t(p) : minus_t(p);
     merge_equivalent(t, nullptr, err);
     if (err.code) return {};
-    return up ? upgrade_merged(t, L, err) : degrade_merged(t, L, nullptr, err);
+    return up ? upgrade_merged(t, L, err, nullptr) : degrade_merged(t, L, nullptr, err);
 }
 
 double error_prob(const std::vector<Letter>& p) {
@@ -449,7 +462,10 @@ int tree(std::vector<Letter> root, int n, int64_t L, bool up, int threads, doubl
     return 0;
 }
 
-}  // namespace
+}  // namespace tv
+}  // namespace pcub
+
+using namespace pcub::tv;
 
 extern "C" int pcub_bmd_merge_equivalent(const double* probs, int64_t n, double* out, int64_t* out_n,
                                          int64_t* group) {
@@ -479,7 +495,7 @@ extern "C" int pcub_bmd_degrade(const double* merged, int64_t n, int64_t L, doub
 extern "C" int pcub_bmd_upgrade(const double* merged, int64_t n, int64_t L, double* out, int64_t* out_n) {
     if (n < 1 || L < 1 || !merged || !out || !out_n) return PCUB_EINVAL;
     Err err;
-    std::vector<Letter> o = upgrade_merged(load(merged, n), L, err);
+    std::vector<Letter> o = upgrade_merged(load(merged, n), L, err, nullptr);
     if (err.code) return err.code;
     store(o, out, out_n);
     return 0;

@@ -1,16 +1,29 @@
-"""Scalar q-ary channels and the vector factory feeding the q-ary decoder.
+"""Scalar q-ary channels, the vector factory feeding the q-ary decoder, and the q-ary
+degrading/upgrading code construction.
 
-Counterpart of ScalarDistributions/QaryMemorylessDistribution.py for the hot
-path: probs[y][x], calcXMarginals (:155-172),
-probXGivenY (:174-175), makeQaryMemorylessVectorDistribution (:757-776),
-makeQSC (:780-784), makeQEC (:787-798).  The degrading/upgrading construction
-(:400-991) is not part of the decode path.
+Counterpart of ScalarDistributions/QaryMemorylessDistribution.py with the reference's names:
+probs[y][x], calcXMarginals (:155-165), probXGivenY (:174-175), calcYMarginal (:177-179),
+errorProb / conditionalEntropy / totalVariation (:53-96), minusTransform / plusTransform
+(:182-212), degrade / upgrade (dynamic, :215-475), removeZeroProbOutput / normalize
+(:708-751), calcMFromL (:753-755), makeQaryMemorylessVectorDistribution (:757-776),
+makeQSC / makeQEC / makeInputDistribution (:780-811), and the construction
+calcFrozenSet_degradingUpgrading / calcTVAndPe_degradingUpgrading with its .npy cache
+(:910-991).  degrade / upgrade and the tree run in the native host library
+(polarcub_amd.construction, csrc/host/qary_construct.cpp), bit-identical to the reference.
 """
 import math
+import os
 
 import numpy as np
 
-from . import vectors
+from . import construction, vectors
+
+
+def eta(p):
+    """-p log2 p (ScalarDistributions/BinaryMemorylessDistribution.py:451-459)."""
+    assert 0.0 <= p <= 1.0 + 10 * 2.220446049250313e-16
+    p = min(1.0, p)
+    return 0.0 if p == 0.0 else -p * math.log2(p)
 
 
 def eta_list(probs):
@@ -18,12 +31,47 @@ def eta_list(probs):
 
 
 class QaryMemorylessDistribution:
-    def __init__(self, q):
+    def __init__(self, q, use_log=False):
         self.q = q
+        self.use_log = use_log
         self.probs = []  # probs[yindex][xindex]
+
+    def __str__(self):
+        rows = ", ".join("[" + ", ".join(str(p) for p in row) + "]" for row in self.probs)
+        return ("Qry memoryless channel with q = " + str(self.q) + " and " + str(len(self.probs))
+                + " output symbols. The error probability is " + str(self.errorProb())
+                + ". The conditional entropy is " + str(self.conditionalEntropy())
+                + ". [p(y,x=0), p(y,x=1), ..., p(y,x=q-1)]: " + rows)
 
     def append(self, item):
         self.probs.append(item)
+
+    def calcOutputAlphabetSize(self):
+        return len(self.probs)
+
+    # -- polar toolbox ---------------------------------------------------------
+    def errorProb(self):
+        total = 0.0
+        for row in self.probs:
+            t = sorted(row)
+            total += sum(t[:-1])
+        return total
+
+    def conditionalEntropy(self):
+        s = 0.0
+        for row in self.probs:
+            for p in row:
+                s += eta(p)
+            s -= eta(sum(row))
+        return s
+
+    def totalVariation(self):
+        s = 0.0
+        for row in self.probs:
+            for p1 in row:
+                for p2 in row:
+                    s += abs(p1 - p2)
+        return s / (2 * (self.q - 1))
 
     def calcXMarginals(self):
         out = []
@@ -34,18 +82,72 @@ class QaryMemorylessDistribution:
             out.append(s)
         return out
 
+    def calcXMarginal(self, x):
+        s = 0.0
+        for row in self.probs:
+            s += row[x]
+        return s
+
     def probXGivenY(self, x, y):
         return self.probs[y][x] / sum(self.probs[y])
 
     def calcYMarginal(self, y):
         return sum(self.probs[y])
 
-    def errorProb(self):
-        return sum(sum(row) - max(row) for row in self.probs)
+    def minusTransform(self):
+        q = self.q
+        new = QaryMemorylessDistribution(q)
+        for y1 in self.probs:
+            for y2 in self.probs:
+                t = [0 for _ in range(q)]
+                for x1 in range(q):
+                    for x2 in range(q):
+                        t[(x1 + x2) % q] += y1[x1] * y2[x2]
+                new.append(t)
+        return new
+
+    def plusTransform(self):
+        q = self.q
+        new = QaryMemorylessDistribution(q)
+        for y1 in self.probs:
+            for y2 in self.probs:
+                for u1 in range(q):
+                    t = [0 for _ in range(q)]
+                    for u2 in range(q):
+                        t[u2] += y1[(u1 - u2 + q) % q] * y2[u2]
+                    new.append(t)
+        return new
+
+    # -- degrading / upgrading (native) ------------------------------------------
+    def _from_rows(self, rows):
+        new = QaryMemorylessDistribution(self.q)
+        new.probs = [list(map(float, r)) for r in rows]
+        return new
+
+    def degrade(self, L):
+        return self.degrade_dynamic(L)
+
+    def degrade_dynamic(self, L):
+        return self._from_rows(construction.qmd_degrade(self.q, self.probs, L))
+
+    def upgrade(self, L):
+        return self.upgrade_dynamic(L)
+
+    def upgrade_dynamic(self, L):
+        return self._from_rows(construction.qmd_upgrade(self.q, self.probs, L))
+
+    def removeZeroProbOutput(self):
+        self.probs = [row for row in self.probs if sum(row) > 0.0]
 
     def normalize(self):
-        s = sum(sum(row) for row in self.probs)
+        flat = sorted(p for row in self.probs for p in row)
+        s = 0.0
+        for p in flat:
+            s += p
         self.probs = [[p / s for p in row] for row in self.probs]
+
+    def calcMFromL(self, L):
+        return construction.calc_m(self.q, L)
 
     def makeQaryMemorylessVectorDistribution(self, length, yvec, use_log=False):
         vd = vectors.QaryMemorylessVectorDistribution(self.q, length, use_log)
@@ -72,3 +174,73 @@ def makeQEC(q, p):
         qec.append([(1.0 - p) / q if x == y else 0.0 for x in range(q)])
     qec.append([p / q for _ in range(q)])
     return qec
+
+
+def makeInputDistribution(probs):
+    dist = QaryMemorylessDistribution(len(probs))
+    dist.append(list(probs))
+    dist.normalize()
+    return dist
+
+
+def _cache_names(directory_name, L):
+    base = directory_name + "DegradingUpgrading_L=" + str(L)
+    return base + "_tv.npy", base + "_pe.npy"
+
+
+def calcTVAndPe_degradingUpgrading(n, L, xDistribution, xyDistribution, directory_name=None, verbosity=False,
+                                   threads=0):
+    """TV / Pe vectors of the degraded xy tree and upgraded x tree (:934-991).  With a
+    directory_name the reference's .npy cache is read if both files exist, else written
+    (directory_name + 'DegradingUpgrading_L=<L>_tv.npy' / '_pe.npy').  Without one the
+    reference returns None (and calcFrozenSet_degradingUpgrading then fails); here the
+    vectors are computed and returned uncached."""
+    if directory_name is not None:
+        tv_name, pe_name = _cache_names(directory_name, L)
+        if verbosity:
+            print(tv_name)
+            print(pe_name)
+        if os.path.isfile(tv_name) and os.path.isfile(pe_name):
+            return np.load(tv_name), np.load(pe_name)
+        if verbosity:
+            print("Calculating TV and Pe vectors...")
+    q = xyDistribution.q
+    TV, Pe = construction.qary_tv_pe(q, n, L, None if xDistribution is None else xDistribution.probs,
+                                     xyDistribution.probs, threads)
+    TVvec, Pevec = [float(v) for v in TV], [float(v) for v in Pe]
+    if directory_name is None:
+        return TVvec, Pevec
+    if verbosity:
+        print("Done calculating!")
+    if not os.path.exists(directory_name):
+        os.makedirs(directory_name)
+    np.save(tv_name, TVvec)
+    np.save(pe_name, Pevec)
+    return TVvec, Pevec
+
+
+def calcFrozenSet_degradingUpgrading(n, L, xDistribution, xyDistribution, directory_name=None,
+                                     upperBoundOnErrorProbability=None, numInfoIndices=None, verbosity=False):
+    """Frozen set from the degrading/upgrading construction (:910-932) through
+    QaryPolarEncoderDecoder.frozenSetFromTVAndPe."""
+    from . import coding_qary
+    assert n >= 0
+    assert L > 0
+    assert upperBoundOnErrorProbability is None or upperBoundOnErrorProbability > 0
+    assert xyDistribution is not None
+    TVvec, Pevec = calcTVAndPe_degradingUpgrading(n, L, xDistribution, xyDistribution, directory_name,
+                                                  verbosity=verbosity)
+    return coding_qary.frozenSetFromTVAndPe(TVvec, Pevec, upperBoundOnErrorProbability, numInfoIndices,
+                                            verbosity=verbosity)
+
+
+def degrade_dynamic_upper_bound(q, L):
+    """Equation (27) of Ordentlich-Tal, in bits (:876-882)."""
+    M = construction.calc_m(q, L)
+    return (64 * (q - 1) / (M ** 2)) / math.log(2)
+
+
+def upgrade_dynamic_upper_bound(q, L):
+    """Equation (13) of Ordentlich-Tal, in bits (:885-891)."""
+    M = construction.calc_m(q, L)
+    return (128 * (q - 1) / (M ** 2)) / math.log(2)

@@ -73,18 +73,33 @@ PCUB_HD int first_frozen_depth(const uint32_t* fmask, int k, int D, int SU) {
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// Exchange with lane ^ MASK.  Within a quad (MASK 1, 2) this is a DPP quad_perm
-// move (a VALU op, no LDS round trip: the cross-lane leaf chains are serial, so
-// the ds_bpermute latency is on the critical path); wider masks use __shfl_xor.
-// Every caller exchanges inside an aligned group of >= 2*MASK lanes that share
-// their control flow, so the source lane is always active.
+// Exchange with lane ^ MASK.  Inside a row of 16 lanes this is DPP (VALU moves, no
+// LDS round trip: the cross-lane leaf chains are serial, so the ds_bpermute latency
+// is on the critical path): MASK 1, 2 a quad_perm; MASK 8 the row rotation by 8;
+// MASK 4 the rotation by 12 (row_ror:k gives lane i the value of lane i - k mod 16),
+// then banks 1 and 3 of the row (lanes 4-7, 12-15) overwritten by the rotation by 4
+// (checked on the GPU by tests/emu/dpp_check.hip).  Wider masks use __shfl_xor.  Every caller
+// exchanges inside an aligned group of >= 2*MASK lanes that share their control
+// flow, so the source lane is always active.
+template <int CTRL, int BANKS = 0xF>
+PCUB_HD unsigned dpp32(unsigned old, unsigned src) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)src, CTRL, 0xF, BANKS, false);
+}
+
+template <int MASK>
+PCUB_HD unsigned xor_lane32(unsigned x) {
+    if constexpr (MASK == 1) return dpp32<0xB1>(0u, x);         // quad_perm [1,0,3,2]
+    else if constexpr (MASK == 2) return dpp32<0x4E>(0u, x);    // quad_perm [2,3,0,1]
+    else if constexpr (MASK == 8) return dpp32<0x128>(0u, x);   // row_ror:8
+    else return dpp32<0x124, 0xA>(dpp32<0x12C>(0u, x), x);      // row_ror:12, banks 1,3: row_ror:4
+}
+
 template <int MASK>
 PCUB_HD double xor_shfl_c(double v) {
-    if constexpr (MASK == 1 || MASK == 2) {
-        constexpr int ctrl = (MASK == 1) ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+    if constexpr (MASK == 1 || MASK == 2 || MASK == 4 || MASK == 8) {
         const unsigned long long b = (unsigned long long)as_bits(v);
-        const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, ctrl, 0xF, 0xF, false);
-        const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), ctrl, 0xF, 0xF, false);
+        const unsigned lo = xor_lane32<MASK>((unsigned)b);
+        const unsigned hi = xor_lane32<MASK>((unsigned)(b >> 32));
         return from_bits((long long)(((unsigned long long)hi << 32) | lo));
     } else {
         return __shfl_xor(v, MASK);

@@ -126,6 +126,18 @@ int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, i
                           int32_t ones, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
                           const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
                           double* leaf, void* stream);
+/* q-ary SC in the log domain (QaryPolarEncoderDecoder(..., use_log=True).decode,
+ * QaryPolarEncoderDecoder.py:318-401 over VectorDistributions/QaryMemorylessVectorDistribution.py
+ * with use_log): logaddexp minus transform, logsumexp normalisation and marginal.
+ *   xy    [N][B][q] f64 log-probabilities (-inf allowed); q in 2..8, log2N in 1..16
+ *   info  [K][B] u8 symbols; xhat [N][B] u8 or NULL; leaf [N][B][q] f64 log marginals or NULL
+ * Device exp/log1p/log: values agree with the reference within a few ulps (not bit-exact).
+ * Workspace: pcub_sc_decode_qary_log_workspace(B, q, log2N) bytes. */
+size_t pcub_sc_decode_qary_log_workspace(int64_t B, int32_t q, int32_t log2N);
+int pcub_sc_decode_qary_log(const double* xy, int64_t B, int32_t q, int32_t log2N, const uint32_t* frozen_mask,
+                            int32_t K, uint8_t* info, uint8_t* xhat, double* leaf, void* workspace,
+                            size_t workspace_bytes, void* stream);
+
 /* Non-uniform a-priori distribution (two trees).  Replaces recursiveEncodeDecode with an
  * xVectorDistribution that is not uniform (BinaryPolarEncoderDecoder.py:223-325, called by
  * decode :71-99 and encode :46-69): the prior tree px runs beside the xy tree through the same

@@ -1040,9 +1040,14 @@ def fx_qary_log(R, timing):
     orig = cls.calcMarginalizedProbabilities
     out, meta = {}, []
     rs = np.random.default_rng(31)
-    for name, q, n, p, T in (("q4_n6", 4, 6, 0.11, 40), ("q3_n5", 3, 5, 0.2, 40), ("q2_n4", 2, 4, 0.11, 24)):
+    cq = np.load(os.path.join(OUT, "construct_qary.npz"))
+    for name, q, n, p, T in (("q4_n6", 4, 6, 0.11, 40), ("q3_n5", 3, 5, 0.2, 40), ("q2_n4", 2, 4, 0.11, 24),
+                             ("q4_n5_good", 4, 5, 0.11, 40)):
         N = 1 << n
-        frozen = set(int(i) for i in rs.permutation(N)[:N // 2])
+        if name.endswith("_good"):  # the reference construction's frozen set (qsc4_n5_L64, K=16)
+            frozen = set(int(i) for i in np.nonzero(cq["qsc4_n5_L64_frozen"])[0])
+        else:
+            frozen = set(int(i) for i in rs.permutation(N)[:N // 2])
         dec = QPED.QaryPolarEncoderDecoder(q, N, frozen, 1, use_log=True)
         qsc = QMD.makeQSC(q, p)
         xd = QMD.QaryMemorylessDistribution(q)

@@ -11,9 +11,13 @@
 decode() of a linear-domain QaryMemorylessVectorDistribution (2 <= q <= 8,
 N >= 4) runs on the GPU (pcub_sc_decode_qary), bit-identical to the
 reference; the a-priori tree never influences q-ary decisions (frozen symbols
-are 0), so any prior is accepted.  Other plugins and the log domain use the
-generic recursion over the plugin's own methods.  List decoding and the IR
-simulation (:118-227, :403-930) are not part of this module.
+are 0), so any prior is accepted.  decode() of a log-domain (use_log=True)
+memoryless distribution (2 <= q <= 8, 2 <= N <= 2^16) runs on the GPU log-domain
+kernel (pcub_sc_decode_qary_log: numpy's logaddexp and scipy's logsumexp restated
+over the device's exp/log1p/log, so within a few ulps of the reference rather than
+bit-identical).  Other plugins use the generic recursion over the plugin's own
+methods.  List decoding and the IR simulation (:118-227, :403-930) are not part of
+this module.
 """
 import random
 
@@ -62,6 +66,20 @@ class QaryPolarEncoderDecoder:
     def _device_ok(self):
         return 2 <= self.q <= 8 and self.length >= 4
 
+    def _log_device(self):
+        from . import sc
+        if getattr(self, "_logdev", None) is None:
+            self._logdev = sc.QaryLogDecoder(self.q, self.length, self._mask)
+        return self._logdev
+
+    def decode_log_batch(self, xy):
+        """xy: [B, N, q] log-domain rows (use_log=True) -> information int64[B, k]."""
+        import torch
+        dec = self._log_device()
+        t = xy if isinstance(xy, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(xy, np.float64))
+        info, _ = dec.decode(t.to(dec.device, torch.float64))
+        return info.cpu().numpy().astype(np.int64)
+
     def decode_batch(self, xy):
         """xy: [B, N, q] linear-domain joint probabilities -> information int64[B, k]."""
         import torch
@@ -94,6 +112,11 @@ class QaryPolarEncoderDecoder:
             p = np.asarray(xyVectorDistribution.probs, dtype=np.float64)
             assert np.all(p >= 0) and np.all(np.isfinite(p)), "probabilities must be finite and non-negative"
             return self.decode_batch(p[None])[0]
+        if (2 <= self.q <= 8 and 2 <= self.length <= 1 << 16 and _is_qary_memoryless(xyVectorDistribution)
+                and getattr(xyVectorDistribution, "use_log", False)):
+            p = np.asarray(xyVectorDistribution.probs, dtype=np.float64)
+            assert not np.any(np.isnan(p)) and not np.any(p == np.inf), "log-probabilities must be < +inf"
+            return self.decode_log_batch(p[None])[0]
         information = np.full(self.k, -1, dtype=np.int64)
         (enc, nu, ni) = self.recursiveEncodeDecode(information, 0, 0, xVectorDistribution, xyVectorDistribution)
         assert nu == len(enc) == self.length and ni == self.k

@@ -418,6 +418,53 @@ class QaryDecoder:
         return info.t().contiguous(), xh.t().contiguous()
 
 
+class QaryLogDecoder:
+    """Batched q-ary SC in the log domain (pcub_sc_decode_qary_log): use_log=True vector
+    distributions, log-probabilities in, symbols and log leaf marginals out.  Values agree
+    with the reference within a few ulps (device exp/log1p/log), decisions exactly wherever
+    no two marginals are that close."""
+
+    def __init__(self, q, N, frozen_mask, device=None):
+        self.q = int(q)
+        if not 2 <= self.q <= 8:
+            raise ValueError("q must be in [2, 8] for the device decoder")
+        self.N = int(N)
+        self.n = _log2(self.N)
+        if not 1 <= self.n <= 16:
+            raise ValueError("log-domain device decoder needs 2 <= N <= 2^16")
+        mask = (np.asarray(frozen_mask, dtype=np.uint8).reshape(-1) != 0).astype(np.uint8)
+        if mask.shape[0] != self.N:
+            raise ValueError("frozen mask has %d entries, expected N=%d" % (mask.shape[0], self.N))
+        self.K = int(self.N - int(mask.sum()))
+        self.device = torch.device("cuda") if device is None else torch.device(device)
+        self.fwords = torch.from_numpy(pack_rows(mask).reshape(-1).view(np.int32).copy()).to(self.device)
+        self._ws = None
+
+    def decode_native(self, xy, want_xhat=True, want_leaf=False):
+        """xy [N, B, q] log-probabilities (device) -> (info [K, B] u8, xhat [N, B] u8 | None,
+        leaf [N, B, q] f64 | None)."""
+        if xy.dtype != torch.float64 or xy.dim() != 3 or xy.shape[0] != self.N or xy.shape[2] != self.q:
+            raise ValueError("xy must be float64 [N, B, q] with N=%d, q=%d" % (self.N, self.q))
+        xy = xy.contiguous()
+        B = xy.shape[1]
+        need = int(_lib.lib().pcub_sc_decode_qary_log_workspace(B, self.q, self.n))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 16), dtype=torch.uint8, device=xy.device)
+        info = torch.empty((max(1, self.K), B), dtype=torch.uint8, device=xy.device)
+        xh = torch.empty((self.N, B), dtype=torch.uint8, device=xy.device) if want_xhat else None
+        leaf = torch.empty((self.N, B, self.q), dtype=torch.float64, device=xy.device) if want_leaf else None
+        rc = _lib.lib().pcub_sc_decode_qary_log(_p(xy), B, self.q, self.n, _p(self.fwords), self.K, _p(info), _p(xh),
+                                                _p(leaf), _p(self._ws), self._ws.numel(), _stream())
+        _lib.check(rc, "pcub_sc_decode_qary_log")
+        return info[:self.K], xh, leaf
+
+    def decode(self, xy, want_leaf=False):
+        """xy [B, N, q] -> (info [B, K] u8, xhat [B, N] u8[, leaf log marginals [B, N, q]])."""
+        info, xh, leaf = self.decode_native(transpose_pairs(xy), want_leaf=want_leaf)
+        out = (info.t().contiguous(), xh.t().contiguous())
+        return out + (leaf.transpose(0, 1).contiguous(),) if want_leaf else out
+
+
 def encode_qary(code, info):
     """info [B, K] uint8 symbols -> codewords [B, N] uint8."""
     B = info.shape[0]

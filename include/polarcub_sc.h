@@ -138,6 +138,24 @@ int pcub_sc_decode_qary_log(const double* xy, int64_t B, int32_t q, int32_t log2
                             int32_t K, uint8_t* info, uint8_t* xhat, double* leaf, void* workspace,
                             size_t workspace_bytes, void* stream);
 
+/* q-ary SCL / Fast-SSC list decoding (QaryPolarEncoderDecoder.listDecode,
+ * QaryPolarEncoderDecoder.py:118-227, 403-820; rate-0, repetition, rate-1 and single-parity-check
+ * nodes as the reference), linear domain, one lane per codeword.
+ *   xy           [N][B][q] f64; q in 2..8, log2N in 0..12, L (maxListSize) in 1..64
+ *   frozen       [N] u8 (1 = frozen); frozen_vals [nF][B] u8 frozen values in frozen-index order
+ *   actual       [K][B] u8 actual information (listDecode's actualInformation) or NULL
+ *   out_info     [L][K][B] u8 final list (rows >= out_size: 0xff); out_prob [L][B] f64 metrics
+ *                (normalised to max 1); out_size [B]; out_actual [B] actual_prob (with actual)
+ * Ties among candidate metrics / reliabilities go to the lower index and the list is kept in
+ * ascending candidate order (the reference's order comes from numpy's argpartition, which is
+ * CPU-dependent); without ties the final path set and metrics are the reference's.
+ * Workspace: pcub_scl_qary_workspace(B, q, log2N, L, K) bytes. */
+size_t pcub_scl_qary_workspace(int64_t B, int32_t q, int32_t log2N, int32_t L, int32_t K);
+int pcub_scl_qary(const double* xy, int64_t B, int32_t q, int32_t log2N, int32_t L, const uint8_t* frozen,
+                  const uint8_t* frozen_vals, int32_t nF, const uint8_t* actual, int32_t K, uint8_t* out_info,
+                  double* out_prob, int32_t* out_size, double* out_actual, void* workspace, size_t workspace_bytes,
+                  void* stream);
+
 /* Non-uniform a-priori distribution (two trees).  Replaces recursiveEncodeDecode with an
  * xVectorDistribution that is not uniform (BinaryPolarEncoderDecoder.py:223-325, called by
  * decode :71-99 and encode :46-69): the prior tree px runs beside the xy tree through the same

@@ -1031,6 +1031,97 @@ def fx_combine_codes(R, timing):
          out=np.array(out))
 
 
+def fx_scl(R, timing):
+    """The reference's q-ary list decoder (QaryPolarEncoderDecoder.listDecode / recursiveListDecode,
+    :118-227, 403-820) on tie-free inputs (continuous random rows, no zeros), with an actual
+    information word: the final list (informationList[:finalListSize], captured from the
+    outermost recursiveListDecode return), prob_list, actual_prob and the returned ProbResult.
+    The list ORDER is numpy-argpartition-dependent; tests compare it as a set."""
+    QPED = R["QPED"]
+    rs = np.random.default_rng(404)
+    out, cases = {}, []
+    specs = [(2, 3, 2, 0.5), (2, 4, 4, 0.5), (3, 3, 2, 0.4), (3, 4, 4, 0.5), (4, 3, 4, 0.5), (4, 4, 8, 0.5),
+             (2, 5, 8, 0.6), (3, 5, 3, 0.5), (4, 5, 4, 0.6), (2, 4, 1, 0.5), (4, 4, 16, 0.3), (3, 3, 8, 0.2)]
+    for ci, (q, n, L, fr) in enumerate(specs):
+        N = 1 << n
+        frozen = set(int(i) for i in np.nonzero(rs.random(N) < fr)[0])
+        dec = QPED.QaryPolarEncoderDecoder(q, N, frozen, 1)
+        T = 12
+        K = dec.k
+        xy = rs.random((T, N, q)) * 0.98 + 0.02
+        fv = rs.integers(0, q, (T, len(frozen)))
+        act = rs.integers(0, q, (T, K))
+        infos = np.full((T, L, K), -1, np.int64)
+        probs = np.full((T, L), np.nan)
+        sizes = np.zeros(T, np.int64)
+        aprob = np.zeros(T)
+        ret = np.zeros((T, K), np.int64)
+        pres = []
+        for t in range(T):
+            vd = R["QMVD"].QaryMemorylessVectorDistribution(q, N)
+            vd.probs[:] = xy[t]
+            orig = dec.recursiveListDecode
+            depth = [0]
+            top = {}
+
+            def wrapped(*a, _orig=orig, **k):
+                depth[0] += 1
+                try:
+                    r = _orig(*a, **k)
+                finally:
+                    depth[0] -= 1
+                if depth[0] == 0:
+                    top["r"] = r
+                return r
+            dec.recursiveListDecode = wrapped
+            try:
+                info, pr = dec.listDecode(vd, fv[t], L, np.zeros((K, 0), np.int64), np.zeros(0, np.int64),
+                                          actualInformation=act[t])
+            finally:
+                del dec.recursiveListDecode
+            il, _, _, _, fls, _, _ = top["r"]
+            sizes[t] = fls
+            infos[t, :fls] = il[:fls]
+            probs[t, :fls] = dec.prob_list[:fls]
+            aprob[t] = dec.actual_prob
+            ret[t] = info
+            pres.append(pr.name)
+        tag = "c%d" % ci
+        out.update({tag + "_xy": xy, tag + "_frozen": np.array([1 if i in frozen else 0 for i in range(N)], np.uint8),
+                    tag + "_fv": fv.astype(np.uint8), tag + "_actual": act.astype(np.uint8), tag + "_info": infos,
+                    tag + "_prob": probs, tag + "_size": sizes, tag + "_aprob": aprob, tag + "_ret": ret})
+        cases.append(dict(tag=tag, q=q, n=n, L=L, K=K, prob_result=pres))
+    # the reference's irSimulation (:887-930) over a continuous channel (no ties): a q-ary symbol
+    # plus Gaussian noise, likelihood rows exp(-(b - x)^2 / 2 s^2) (build-side closures)
+    import contextlib
+    import io
+    import random as _random
+    irs = []
+    for name, q, n, L, T, sig, cs in (("ir_q3_n4", 3, 4, 4, 60, 0.45, 2), ("ir_q2_n5", 2, 5, 8, 60, 0.6, 1)):
+        N = 1 << n
+        frozen = set(int(i) for i in np.nonzero(np.random.default_rng(9 + q).random(N) < 0.5)[0])
+        chan = _random.Random(1234 + q)
+
+        def simulate(a, _c=chan, _s=sig):
+            return [float(x) + _c.gauss(0.0, _s) for x in a]
+
+        def make_xy(b, _q=q, _s=sig, _N=N):
+            vd = R["QMVD"].QaryMemorylessVectorDistribution(_q, _N)
+            for i, y in enumerate(b):
+                vd.probs[i] = [math.exp(-((y - x) ** 2) / (2 * _s * _s)) for x in range(_q)]
+            return vd
+        np.random.seed(77)
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            fe, se, rate, prl = QPED.irSimulation(q, N, simulate, make_xy, T, frozen, L, cs, verbosity=1)
+        out[name + "_frozen"] = np.array([1 if i in frozen else 0 for i in range(N)], np.uint8)
+        irs.append(dict(name=name, q=q, n=n, L=L, trials=T, sigma=sig, check_size=cs, chan_seed=1234 + q,
+                        np_seed=77, frame_error_prob=fe, symbol_error_prob=float(se), rate=rate,
+                        prob_results=[p.name for p in prl], printed=buf.getvalue()))
+    save("scl", dict(cases=cases, ir=irs, note="listDecode with actualInformation; list order is argpartition's"),
+         **out)
+
+
 def fx_qary_log(R, timing):
     """use_log=True q-ary decodes (VectorDistributions/QaryMemorylessVectorDistribution.py:40,92-118:
     logaddexp transforms, logsumexp normalisation, log-domain marginals): QSC received words and
@@ -1124,6 +1215,7 @@ FIXTURES = {
     "qary_log": fx_qary_log,
     "construct_qary_up": fx_construct_qary_up,
     "combine_codes": fx_combine_codes,
+    "scl": fx_scl,
 }
 
 

@@ -16,10 +16,13 @@ memoryless distribution (2 <= q <= 8, 2 <= N <= 2^16) runs on the GPU log-domain
 kernel (pcub_sc_decode_qary_log: numpy's logaddexp and scipy's logsumexp restated
 over the device's exp/log1p/log, so within a few ulps of the reference rather than
 bit-identical).  Other plugins use the generic recursion over the plugin's own
-methods.  List decoding and the IR simulation (:118-227, :403-930) are not part of
-this module.
+methods.  List decoding (listDecode, :118-227, 403-820) runs on the GPU list decoder
+(pcub_scl_qary, linear domain) and irSimulation / ir (:822-930) batch it; the list's
+tie-breaking and order are documented in include/polarcub_sc.h.
 """
+import math
 import random
+from enum import Enum
 
 import numpy as np
 
@@ -34,6 +37,15 @@ class uIndexType:
 def _is_qary_memoryless(vd):
     return (isinstance(vd, vectors.QaryMemorylessVectorDistribution)
             or (type(vd).__name__ == "QaryMemorylessVectorDistribution" and hasattr(vd, "probs")))
+
+
+class ProbResult(Enum):
+    SuccessActualIsMax = 0
+    SuccessActualSmallerThanMax = 1
+    FailActualLargerThanMax = 2
+    FailActualIsMax = 3
+    FailActualWithinRange = 4
+    FailActualSmallerThanMin = 5
 
 
 class QaryPolarEncoderDecoder:
@@ -122,6 +134,107 @@ class QaryPolarEncoderDecoder:
         assert nu == len(enc) == self.length and ni == self.k
         return information
 
+    # -- list decoding and information reconciliation (:118-242, 822-865) --------------------
+    def list_decode_batch(self, xy, frozenValues, maxListSize, actualInformation=None):
+        """Batched listDecode core on the GPU (pcub_scl_qary): xy [B, N, q] linear-domain rows,
+        frozenValues [B, nF], actualInformation [B, K] or None -> (info [B, L, K] int64 with -1
+        rows past each list's size, prob [B, L], size [B], actual_prob [B] | None)."""
+        from . import sc
+        if not hasattr(self, "_scl"):
+            self._scl = {}
+        dec = self._scl.get(int(maxListSize))
+        if dec is None:
+            dec = self._scl[int(maxListSize)] = sc.QaryListDecoder(self.q, self.length, self._mask, int(maxListSize))
+        info, prob, size, ap = dec.decode(xy, frozenValues, actualInformation)
+        info = info.astype(np.int64)
+        info[info == 0xff] = -1
+        return info, prob, size, ap
+
+    def _list_result(self, infos, probs, size, actual_prob, maxListSize, check_matrix, check_value,
+                     actualInformation):
+        """listDecode's return value from its final list (QaryPolarEncoderDecoder.py:172-227)."""
+        prob_list = probs[:size]
+        if actualInformation is not None:
+            actual = np.asarray(actualInformation)
+            for i, information in enumerate(infos[:maxListSize]):
+                if np.array_equal(information, actual):
+                    return information, (ProbResult.SuccessActualIsMax if prob_list[i] == max(prob_list)
+                                         else ProbResult.SuccessActualSmallerThanMax)
+            mx = max(prob_list)
+            if actual_prob > mx:
+                pr = ProbResult.FailActualLargerThanMax
+            elif actual_prob == mx:
+                pr = ProbResult.FailActualIsMax
+            elif actual_prob >= min(prob_list):
+                pr = ProbResult.FailActualWithinRange
+            else:
+                pr = ProbResult.FailActualSmallerThanMin
+            return infos[0], pr
+        for information in infos[:maxListSize]:
+            if np.array_equal(np.matmul(information, check_matrix) % self.q, check_value):
+                return information, None
+        return infos[0], None
+
+    def listDecode(self, xyVectorDistribution, frozenValues, maxListSize, check_matrix, check_value,
+                   actualInformation=None, verbosity=0):
+        """QaryPolarEncoderDecoder.listDecode (:118-227) on the GPU list decoder; the list's
+        tie-breaking and order are documented in include/polarcub_sc.h."""
+        if getattr(xyVectorDistribution, "use_log", False) or self.use_log:
+            raise NotImplementedError("list decoding runs in the linear domain only (use_log=False)")
+        assert len(xyVectorDistribution) == self.length
+        xy = np.asarray(xyVectorDistribution.probs, dtype=np.float64)[None]
+        act = None if actualInformation is None else np.asarray(actualInformation)[None]
+        info, prob, size, ap = self.list_decode_batch(xy, np.asarray(frozenValues).reshape(1, -1), maxListSize, act)
+        self.prob_list = prob[0, :size[0]]
+        self.actual_prob = None if ap is None else float(ap[0])
+        return self._list_result(info[0], prob[0], int(size[0]), self.actual_prob, maxListSize, check_matrix,
+                                 check_value, actualInformation)
+
+    def mergeInfoAndFrozen(self, actualInformation, frozenValues):
+        merged = np.empty(self.length, dtype=np.int64)
+        merged[list(self.infoSet)] = actualInformation
+        merged[list(self.frozenSet)] = frozenValues
+        return merged
+
+    def calc_explicit_prob(self, information, frozenValues, xyVectorDistribution):
+        guess = polarTransformOfQudits(self.q, self.mergeInfoAndFrozen(information, frozenValues))
+        vals = [row[guess[i]] for i, row in enumerate(xyVectorDistribution.probs)]
+        return sum(vals) if self.use_log else np.prod(vals)
+
+    def calculate_syndrome_and_complement(self, u_message):
+        y = polarTransformOfQudits(self.q, u_message)
+        w = np.copy(y)
+        w[list(self.infoSet)] = 0
+        w[list(self.frozenSet)] *= self.q - 1
+        w[list(self.frozenSet)] %= self.q
+        u = y
+        u[list(self.frozenSet)] = 0
+        return w, u
+
+    def get_message_info_bits(self, u_message):
+        return np.asarray(u_message)[list(self.infoSet)]
+
+    def get_message_frozen_bits(self, u_message):
+        return np.asarray(u_message)[list(self.frozenSet)]
+
+    def _ir_inputs(self, a, b, make_xyVectorDistribution, check_size):
+        """ir()'s preparation (:841-855), consuming the global numpy RNG as the reference does."""
+        w, u = self.calculate_syndrome_and_complement(a)
+        a_key = self.get_message_info_bits(u)
+        frozen_values = (self.get_message_frozen_bits(w) * (self.q - 1)) % self.q
+        check_matrix = np.random.choice(range(self.q), (self.k, check_size))
+        check_value = np.matmul(a_key, check_matrix) % self.q
+        xyvd = make_xyVectorDistribution(b)
+        return a_key, frozen_values, check_matrix, check_value, xyvd
+
+    def ir(self, a, b, make_xyVectorDistribution, list_size=1, check_size=0, verbosity=0):
+        """Information reconciliation of one pair (:841-858)."""
+        a_key, frozen_values, check_matrix, check_value, xyvd = self._ir_inputs(a, b, make_xyVectorDistribution,
+                                                                                check_size)
+        b_key, prob_result = self.listDecode(xyvd, frozen_values, list_size, check_matrix, check_value,
+                                             actualInformation=a_key, verbosity=verbosity)
+        return a_key, b_key, prob_result
+
     def recursiveEncodeDecode(self, information, uIndex, informationVectorIndex, xVectorDistribution,
                               xyVectorDistribution=None, marginalizedUProbs=None):
         """Generic q-ary SC recursion over plugin methods (QaryPolarEncoderDecoder.py:318-401)."""
@@ -196,6 +309,57 @@ def encodeDecodeSimulation(q, length, make_xVectorDistribution, make_codeword, s
             if not np.array_equal(infos[t], decoded[t]):
                 errors += 1
     print("Error probability = ", errors, "/", numberOfTrials, " = ", errors / numberOfTrials)
+
+
+def hamming(x, y):
+    return sum(np.asarray(x) != np.asarray(y))
+
+
+def irSimulation(q, length, simulateChannel, make_xyVectorDistribution, numberOfTrials, frozenSet, maxListSize=1,
+                 checkSize=0, commonRandomnessSeed=1, randomInformationSeed=1, use_log=False, verbosity=0,
+                 ir_version=1, chunk=4096):
+    """Information-reconciliation simulation (QaryPolarEncoderDecoder.py:887-930), batched: the
+    per-trial draws (information RNG, the channel closure, the global numpy RNG of the check
+    matrix) run on the host in trial order exactly as the reference consumes them, the list
+    decodes run on the GPU in chunks.  Returns (frame_error_prob, symbol_error_prob, rate,
+    probResultList) and prints the reference's lines when verbosity is set."""
+    if ir_version != 1:
+        raise TypeError("ir2 (ir_version=2) fails in the reference itself (listDecode argument mismatch)")
+    encDec = QaryPolarEncoderDecoder(q, length, frozenSet, commonRandomnessSeed, use_log=use_log)
+    if use_log:
+        raise NotImplementedError("list decoding runs in the linear domain only (use_log=False)")
+    informationRNG = random.Random(randomInformationSeed)
+    badKeys = badSymbols = 0
+    probResultList = []
+    a_key = None
+    for t0 in range(0, numberOfTrials, chunk):
+        T = min(chunk, numberOfTrials - t0)
+        keys, fvs, xys = [], [], []
+        for _ in range(T):
+            a = informationRNG.choices(range(0, q), k=encDec.length)
+            b = simulateChannel(a)
+            a_key, fv, _, _, xyvd = encDec._ir_inputs(a, b, make_xyVectorDistribution, checkSize)
+            keys.append(a_key)
+            fvs.append(fv)
+            xys.append(np.asarray(xyvd.probs, dtype=np.float64))
+        info, prob, size, ap = encDec.list_decode_batch(np.stack(xys), np.stack(fvs), maxListSize, np.stack(keys))
+        for t in range(T):
+            b_key, pr = encDec._list_result(info[t], prob[t], int(size[t]), float(ap[t]), maxListSize, None, None,
+                                            keys[t])
+            probResultList.append(pr)
+            if not np.array_equal(keys[t], b_key):
+                badKeys += 1
+                badSymbols += hamming(keys[t], b_key)
+    assert len(a_key) == length - len(frozenSet)
+    rate = (math.log2(q) * len(a_key) - math.log2(maxListSize)) / length
+    frame_error_prob = badKeys / numberOfTrials
+    symbol_error_prob = badSymbols / (numberOfTrials * encDec.length)
+    if verbosity:
+        print("Rate: ", rate)
+        print("Frame error probability = ", badKeys, "/", numberOfTrials, " = ", frame_error_prob)
+        print("Symbol error probability = ", badSymbols, "/ (", numberOfTrials, " * ", encDec.length, ") = ",
+              symbol_error_prob)
+    return frame_error_prob, symbol_error_prob, rate, probResultList
 
 
 def polarTransformOfQudits(q, xvec):

@@ -465,6 +465,62 @@ class QaryLogDecoder:
         return out + (leaf.transpose(0, 1).contiguous(),) if want_leaf else out
 
 
+class QaryListDecoder:
+    """Batched q-ary SCL / Fast-SSC list decoding (pcub_scl_qary): QaryPolarEncoderDecoder.listDecode
+    for B codewords of one code at list size L, with optional actual information words."""
+
+    def __init__(self, q, N, frozen_mask, L, device=None):
+        self.q, self.N, self.L = int(q), int(N), int(L)
+        self.n = _log2(self.N)
+        if not 2 <= self.q <= 8 or not 1 <= self.L <= 64 or self.n > 12:
+            raise ValueError("list decoder needs 2 <= q <= 8, 1 <= L <= 64, N <= 4096")
+        mask = (np.asarray(frozen_mask, dtype=np.uint8).reshape(-1) != 0).astype(np.uint8)
+        if mask.shape[0] != self.N:
+            raise ValueError("frozen mask has %d entries, expected N=%d" % (mask.shape[0], self.N))
+        self.K = int(self.N - int(mask.sum()))
+        self.nF = self.N - self.K
+        self.device = torch.device("cuda") if device is None else torch.device(device)
+        self.frozen_dev = torch.from_numpy(mask.copy()).to(self.device)
+        self._ws = None
+
+    def decode_native(self, xy, frozen_vals, actual=None):
+        """xy [N, B, q] f64, frozen_vals [nF, B] u8, actual [K, B] u8 or None (device tensors)
+        -> (info [L, K, B] u8, prob [L, B] f64, size [B] i32, actual_prob [B] f64 | None)."""
+        if xy.dtype != torch.float64 or xy.dim() != 3 or xy.shape[0] != self.N or xy.shape[2] != self.q:
+            raise ValueError("xy must be float64 [N, B, q] with N=%d, q=%d" % (self.N, self.q))
+        xy = xy.contiguous()
+        B = xy.shape[1]
+        dev = xy.device
+        fv = frozen_vals.to(device=dev, dtype=torch.uint8).contiguous() if self.nF else \
+            torch.zeros((1, B), dtype=torch.uint8, device=dev)
+        act = None if actual is None else actual.to(device=dev, dtype=torch.uint8).contiguous()
+        need = int(_lib.lib().pcub_scl_qary_workspace(B, self.q, self.n, self.L, self.K))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 16), dtype=torch.uint8, device=dev)
+        info = torch.empty((self.L, max(1, self.K), B), dtype=torch.uint8, device=dev)
+        prob = torch.empty((self.L, B), dtype=torch.float64, device=dev)
+        size = torch.empty(B, dtype=torch.int32, device=dev)
+        ap = torch.empty(B, dtype=torch.float64, device=dev) if act is not None else None
+        rc = _lib.lib().pcub_scl_qary(_p(xy), B, self.q, self.n, self.L, _p(self.frozen_dev), _p(fv), self.nF, _p(act),
+                                      self.K, _p(info), _p(prob), _p(size), _p(ap), _p(self._ws), self._ws.numel(),
+                                      _stream())
+        _lib.check(rc, "pcub_scl_qary")
+        return info[:, :self.K], prob, size, ap
+
+    def decode(self, xy, frozen_vals, actual=None):
+        """xy [B, N, q], frozen_vals [B, nF], actual [B, K] or None -> numpy (info [B, L, K],
+        prob [B, L], size [B], actual_prob [B] | None)."""
+        dev = self.device
+        x = transpose_pairs(torch.as_tensor(np.ascontiguousarray(xy, np.float64), device=dev))
+        fv = torch.as_tensor(np.ascontiguousarray(np.asarray(frozen_vals, np.uint8).reshape(-1, self.nF).T),
+                             device=dev)
+        act = None if actual is None else torch.as_tensor(
+            np.ascontiguousarray(np.asarray(actual, np.uint8).reshape(-1, self.K).T), device=dev)
+        info, prob, size, ap = self.decode_native(x, fv, act)
+        return (info.permute(2, 0, 1).cpu().numpy(), prob.t().cpu().numpy(), size.cpu().numpy(),
+                None if ap is None else ap.cpu().numpy())
+
+
 def encode_qary(code, info):
     """info [B, K] uint8 symbols -> codewords [B, N] uint8."""
     B = info.shape[0]

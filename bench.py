@@ -383,6 +383,56 @@ class Qary:
                           % (ncw, reps, cdesc)}
 
 
+class Scl(Qary):
+    """q-ary list decoding (QaryPolarEncoderDecoder.listDecode, pcub_scl_qary) of the q-ary
+    workload's inputs: the same code (C4 frozen set at q=4, N=256) and QSC batch, frozen values 0
+    (the encoder's), list size --list-size; the decoded word is the path of largest metric."""
+    kernel = "k_scl"
+
+    def __init__(self, a, device, rank):
+        super().__init__(a, device, rank)
+        self.L = a.list_size
+        self.ldec = sc.QaryListDecoder(self.q, self.N, self.code.frozen_mask, self.L, device=device)
+        self.fv = torch.zeros((self.N - self.K, self.B), dtype=torch.uint8, device=device)
+        self.outs = None
+
+    def step(self):
+        self.outs = self.ldec.decode_native(self.xy, self.fv)
+
+    def errors(self):
+        info, prob, size, _ = self.outs
+        best = torch.argmax(prob, dim=0)  # [B]
+        sel = info.gather(0, best.view(1, 1, -1).expand(1, info.shape[1], -1))[0]  # [K, B]
+        return mc.error_counts(sel.t(), self.info_tx)
+
+    def tag(self):
+        return "scl_q%d_n%d_L%d" % (self.q, self.n, self.L)
+
+    def describe(self, world):
+        d = super().describe(world)
+        d["metric"] = "list-decoded codewords/sec, q=%d SCL L=%d N=%d QSC(%.2f), batch=%d per GPU" % (
+            self.q, self.L, self.N, self.a.qsc_p, self.B)
+        d["config"]["workload"] = "q-ary SCL / Fast-SSC list decode q=%d N=%d K=%d L=%d QSC(%.2f)" % (
+            self.q, self.N, self.K, self.L, self.a.qsc_p)
+        d["config"]["list_size"] = self.L
+        return d
+
+    def cpu_baseline(self, seconds=10.0):
+        """oracle/scl_oracle.py (pure Python restatement, one core) on a bounded sample."""
+        from oracle import scl_oracle
+        ncw = 16
+        xy = self.xy[:, :ncw, :].permute(1, 0, 2).contiguous().cpu().numpy()
+        fv = [0] * (self.N - self.K)
+        t0 = time.perf_counter()
+        done = 0
+        while done < ncw and time.perf_counter() - t0 < seconds:
+            scl_oracle.list_decode(self.q, self.code.frozen_mask, self.L, xy[done], fv)
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": "codewords/s", "cores": 1, "kind": "port",
+                "sample": "%d codewords of the bench's own inputs, oracle/scl_oracle.py (Python) on 1 core" % done}
+
+
 class Stub:
     """The multi-rank logic of this script on the CPU (gloo): N=64 binary SC over BSC(0.11)
     decoded by the CPU oracle; codeword g's information bits and channel flips are drawn
@@ -431,7 +481,7 @@ class Stub:
                             "batch_per_gpu": self.B, "parallelism": "dp%d over gloo" % world})
 
 
-WORKLOADS = {"awgn": Awgn, "deletion": Deletion, "qary": Qary, "stub": Stub}
+WORKLOADS = {"awgn": Awgn, "deletion": Deletion, "qary": Qary, "scl": Scl, "stub": Stub}
 
 
 def _free_port():
@@ -468,6 +518,7 @@ def build_parser():
     ap.add_argument("--pd", type=float, default=0.1, help="deletion probability")
     ap.add_argument("--xi", type=float, default=0.1, help="guard-band parameter")
     ap.add_argument("--q", type=int, default=4)
+    ap.add_argument("--list-size", type=int, default=8, help="scl: maxListSize")
     ap.add_argument("--qsc-p", type=float, default=0.11)
     ap.add_argument("--qlanes", type=int, default=0, help="q-ary: lanes per codeword (0 = the library's)")
     ap.add_argument("--qregs", type=int, default=0, help="q-ary: cap on register positions per lane (0 = the library's)")

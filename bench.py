@@ -545,11 +545,20 @@ def main(argv=None):
     if world != a.gpus and world > 1:
         log("bench: WORLD_SIZE=%d differs from --gpus %d; reporting the launched world" % (world, a.gpus))
     on_gpu = a.workload != "stub"
+    shared = False
     if on_gpu:
-        device = torch.device("cuda", local if world > 1 else 0)
+        ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+        # more ranks than GPUs (a rehearsal of the multi-rank path on a smaller box): ranks share
+        # devices round-robin and the counters go over gloo (RCCL wants one GPU per rank)
+        shared = world > 1 and int(os.environ.get("LOCAL_WORLD_SIZE", world)) > ndev  # same on every rank
+        device = torch.device("cuda", (local % max(1, ndev)) if world > 1 else 0)
         torch.cuda.set_device(device)
-        if world > 1:
+        if world > 1 and not shared:
             dist.init_process_group("nccl", device_id=device)
+        elif world > 1:
+            dist.init_process_group("gloo")
+            log("rank %d: %d ranks on %d GPU(s): device cuda:%d shared, counters over gloo" % (rank, world, ndev,
+                                                                                         device.index))
         sync = torch.cuda.synchronize
     else:
         device = torch.device("cpu")
@@ -558,7 +567,7 @@ def main(argv=None):
 
         def sync():
             pass
-    coll_dev = device if (on_gpu and world > 1) else None
+    coll_dev = device if (on_gpu and world > 1 and not shared) else None
 
     t0 = time.time()
     w = WORKLOADS[a.workload](a, device, rank)

@@ -43,6 +43,12 @@ PCUB_HD int ek_lbl(uint32_t k) { return (int)(k & 1u); }
 
 template <int LEN, int V, int E>
 struct Trel {
+    // direct-mapped lookups (validated on use, so they are never cleared): vertex index of a
+    // vpos per layer, edge index of (from vertex, to vertex, label) per edge layer.  Without
+    // them every addToEdgeProb is a linear search of the layer's edges, a chain of dependent
+    // private-memory loads on the GPU.  vpos >= VPM (only when a guard-band parse hands a
+    // segment longer than its trellis) falls back to the search.
+    static constexpr int VPM = 2 * V + 2;
     int8_t nv[LEN + 1];     // vertices per layer
     int16_t vp[LEN + 1][V]; // vpos in insertion order
     double pr0[V];          // vertex probabilities of layer 0 (insertion order)
@@ -50,6 +56,8 @@ struct Trel {
     int16_t ne[LEN];        // edges per edge layer
     uint32_t key[LEN][E];   // creation order
     double p[LEN][E];
+    int8_t vidx[LEN + 1][VPM];
+    int16_t lut[LEN][V][V][2];
 
     PCUB_HD void clear() {
         for (int l = 0; l <= LEN; ++l) nv[l] = 0;
@@ -58,9 +66,15 @@ struct Trel {
     // __getVertexAndAddIfNeeded (BinaryTrellis.py:155-162); returns the vertex's index
     PCUB_HD int vertex(int l, int vpos) {
         const int c = nv[l];
-        for (int i = 0; i < c; ++i)
-            if (vp[l][i] == vpos) return i;
+        if (vpos >= 0 && vpos < VPM) {
+            const int i = vidx[l][vpos];
+            if (i >= 0 && i < c && vp[l][i] == vpos) return i;
+        } else {
+            for (int i = 0; i < c; ++i)
+                if (vp[l][i] == vpos) return i;
+        }
         vp[l][c] = (int16_t)vpos;
+        if (vpos >= 0 && vpos < VPM) vidx[l][vpos] = (int8_t)c;
         nv[l] = (int8_t)(c + 1);
         return c;
     }
@@ -77,17 +91,18 @@ struct Trel {
     }
     // addToEdgeProb (BinaryTrellis.py:128-136): from-vertex, to-vertex, then the edge (+= p)
     PCUB_HD void add(int l, int u, int v, int x, double prob) {
-        vertex(l, u);
-        vertex(l + 1, v);
+        const int ui = vertex(l, u);
+        const int vi = vertex(l + 1, v);
         const uint32_t k = ekey(u, v, x);
         const int c = ne[l];
-        for (int i = 0; i < c; ++i)
-            if (key[l][i] == k) {
-                p[l][i] += prob;
-                return;
-            }
+        const int e = lut[l][ui][vi][x];
+        if (e >= 0 && e < c && key[l][e] == k) {
+            p[l][e] += prob;
+            return;
+        }
         key[l][c] = k;
         p[l][c] = 0.0 + prob;
+        lut[l][ui][vi][x] = (int16_t)c;
         ne[l] = (int16_t)(c + 1);
     }
 };

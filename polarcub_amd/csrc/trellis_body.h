@@ -19,6 +19,7 @@
 // in insertion order.  Iterating "vertices of layer i in order, then the edge
 // array filtered by from-vertex" is then the reference's iteration, and all
 // sums are formed in the same order (tests/test_trellis_* pin this bit-exactly).
+// The layers are indexed (Trel::index) so that iteration touches only the vertex's own edges.
 // Vertex probabilities matter only on the first and last layer (the marginal of a
 // length-1 trellis, :260-278); they are kept for those two layers.
 //
@@ -58,6 +59,13 @@ struct Trel {
     double p[LEN][E];
     int8_t vidx[LEN + 1][VPM];
     int16_t lut[LEN][V][V][2];
+    // per edge: from / to vertex index; after index(): the edges of each layer grouped by
+    // from-vertex and by to-vertex, each group in creation order (a stable counting sort), so
+    // "vertices in order, then that vertex's edges in creation order" -- the reference's
+    // iteration -- touches only those edges
+    int8_t efv[LEN][E], etv[LEN][E];
+    int16_t byfrom[LEN][E], byto[LEN][E];
+    int16_t fstart[LEN][V + 1], tstart[LEN][V + 1];
 
     PCUB_HD void clear() {
         for (int l = 0; l <= LEN; ++l) nv[l] = 0;
@@ -102,8 +110,34 @@ struct Trel {
         }
         key[l][c] = k;
         p[l][c] = 0.0 + prob;
+        efv[l][c] = (int8_t)ui;
+        etv[l][c] = (int8_t)vi;
         lut[l][ui][vi][x] = (int16_t)c;
         ne[l] = (int16_t)(c + 1);
+    }
+    // group every edge layer by from-vertex and by to-vertex (structure only: p may change later)
+    PCUB_HD void index() {
+        for (int l = 0; l < LEN; ++l) {
+            const int n = ne[l];
+            for (int v = 0; v <= V; ++v) fstart[l][v] = tstart[l][v] = 0;
+            for (int e = 0; e < n; ++e) {
+                ++fstart[l][efv[l][e] + 1];
+                ++tstart[l][etv[l][e] + 1];
+            }
+            for (int v = 0; v < V; ++v) {
+                fstart[l][v + 1] += fstart[l][v];
+                tstart[l][v + 1] += tstart[l][v];
+            }
+            int16_t fp[V], tp[V];
+            for (int v = 0; v < V; ++v) {
+                fp[v] = fstart[l][v];
+                tp[v] = tstart[l][v];
+            }
+            for (int e = 0; e < n; ++e) {
+                byfrom[l][fp[efv[l][e]]++] = (int16_t)e;
+                byto[l][tp[etv[l][e]]++] = (int16_t)e;
+            }
+        }
     }
 };
 
@@ -154,6 +188,7 @@ PCUB_HD void trellis_build(T& t, const BitF& bit, int s, int m, double pd, const
             }
         }
     }
+    t.index();
 }
 
 // __miusPlusTransform (BinaryTrellis.py:206-258).  dec = nullptr: minus; else bit j
@@ -168,14 +203,15 @@ PCUB_HD void trellis_transform(const P& pt, C& ct, const uint32_t* dec) {
         const int mid = 2 * j + 1;
         const int dj = dec ? (int)((*dec >> j) & 1u) : 0;
         for (int wi = 0; wi < pt.nv[mid]; ++wi) {
-            const int w = pt.vp[mid][wi];
-            for (int a = 0; a < pt.ne[mid - 1]; ++a) {
+            // in-edges of w (layer mid-1, creation order) x out-edges of w (layer mid)
+            for (int ia = pt.tstart[mid - 1][wi]; ia < pt.tstart[mid - 1][wi + 1]; ++ia) {
+                const int a = pt.byto[mid - 1][ia];
                 const uint32_t ka = pt.key[mid - 1][a];
-                if (ek_to(ka) != w) continue;
-                for (int b = 0; b < pt.ne[mid]; ++b) {
+                const double pa = pt.p[mid - 1][a];
+                for (int ib = pt.fstart[mid][wi]; ib < pt.fstart[mid][wi + 1]; ++ib) {
+                    const int b = pt.byfrom[mid][ib];
                     const uint32_t kb = pt.key[mid][b];
-                    if (ek_from(kb) != w) continue;
-                    const double prob = pt.p[mid - 1][a] * pt.p[mid][b];
+                    const double prob = pa * pt.p[mid][b];
                     const int ml = ek_lbl(ka) ^ ek_lbl(kb);
                     if (!dec) {
                         ct.add(j, ek_from(ka), ek_to(kb), ml, prob);
@@ -186,6 +222,7 @@ PCUB_HD void trellis_transform(const P& pt, C& ct, const uint32_t* dec) {
             }
         }
     }
+    ct.index();
 }
 
 // calcNormalizationVector + normalize (BinaryTrellis.py:280-306), as the decoder
@@ -195,11 +232,9 @@ PCUB_HD void trellis_normalize(T& t) {
     for (int i = 0; i < LEN; ++i) {
         double s0 = 0.0, s1 = 0.0;
         for (int vi = 0; vi < t.nv[i]; ++vi) {
-            const int v = t.vp[i][vi];
-            for (int e = 0; e < t.ne[i]; ++e) {
-                const uint32_t k = t.key[i][e];
-                if (ek_from(k) != v) continue;
-                if (ek_lbl(k)) s1 += t.p[i][e];
+            for (int ie = t.fstart[i][vi]; ie < t.fstart[i][vi + 1]; ++ie) {
+                const int e = t.byfrom[i][ie];
+                if (ek_lbl(t.key[i][e])) s1 += t.p[i][e];
                 else s0 += t.p[i][e];
             }
         }
@@ -217,11 +252,10 @@ PCUB_HD void trellis_marginal(const T& t, double& m0, double& m1) {
     m0 = 0.0;
     m1 = 0.0;
     for (int vi = 0; vi < t.nv[0]; ++vi) {
-        const int v = t.vp[0][vi];
         const double pv = t.pr0[vi];
-        for (int e = 0; e < t.ne[0]; ++e) {
+        for (int ie = t.fstart[0][vi]; ie < t.fstart[0][vi + 1]; ++ie) {
+            const int e = t.byfrom[0][ie];
             const uint32_t k = t.key[0][e];
-            if (ek_from(k) != v) continue;
             const double term = pv * t.p[0][e] * t.prob_last(ek_to(k));
             if (ek_lbl(k)) m1 += term;
             else m0 += term;
@@ -243,13 +277,12 @@ PCUB_HD void trellis_collapse(const P& pt, const uint32_t* dec, double& m0, doub
     m1 = 0.0;
     const int dj = dec ? (int)(*dec & 1u) : 0;
     for (int wi = 0; wi < pt.nv[1]; ++wi) {
-        const int w = pt.vp[1][wi];
-        for (int a = 0; a < pt.ne[0]; ++a) {
+        for (int ia = pt.tstart[0][wi]; ia < pt.tstart[0][wi + 1]; ++ia) {
+            const int a = pt.byto[0][ia];
             const uint32_t ka = pt.key[0][a];
-            if (ek_to(ka) != w) continue;
-            for (int b = 0; b < pt.ne[1]; ++b) {
+            for (int ib = pt.fstart[1][wi]; ib < pt.fstart[1][wi + 1]; ++ib) {
+                const int b = pt.byfrom[1][ib];
                 const uint32_t kb = pt.key[1][b];
-                if (ek_from(kb) != w) continue;
                 const double prob = pt.p[0][a] * pt.p[1][b];
                 const int ml = ek_lbl(ka) ^ ek_lbl(kb);
                 int x = ml;

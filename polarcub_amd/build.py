@@ -3,7 +3,7 @@
     python -m polarcub_amd.build [--force]
 
 Compiles every csrc/*.hip translation unit to an object (in parallel, only the
-stale ones: staleness is a sha256 of the source, every header and the flags, stored
+stale ones: staleness is a sha256 of the source, the headers it includes and the flags, stored
 beside each object and the library, never file mtimes) and links polarcub_amd/lib/libpolarcub_hip.so with hipcc; builds the
 host-only construction library polarcub_amd/lib/libpolarcub_construct.so
 (csrc/host/*.cpp) with g++.
@@ -12,6 +12,7 @@ FMA); never build with -ffast-math.
 """
 import hashlib
 import os
+import re
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -87,30 +88,45 @@ def build_host(force=False, verbose=False):
     return HOST_LIB
 
 
-def _headers():
-    out = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    out.append(os.path.join(ROOT, "include", "polarcub_sc.h"))
-    return sorted(out)
+_INCLUDE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+_INC_DIRS = [CSRC, os.path.join(ROOT, "include")]
+
+
+def _headers(src):
+    """The project headers `src` includes, transitively (quoted includes resolved in
+    csrc/ and include/), sorted: a translation unit is rebuilt when one of them changes."""
+    seen, todo = set(), [os.path.join(CSRC, src)]
+    while todo:
+        with open(todo.pop()) as f:
+            text = f.read()
+        for name in _INCLUDE.findall(text):
+            for d in _INC_DIRS:
+                path = os.path.join(d, name)
+                if os.path.exists(path):
+                    if path not in seen:
+                        seen.add(path)
+                        todo.append(path)
+                    break
+    return sorted(seen)
 
 
 def _obj(src):
     return os.path.join(OBJDIR, src.replace(".hip", ".o"))
 
 
-def _obj_digest(src, hdr):
-    return _digest([os.path.join(CSRC, src)] + hdr, [HIPCC, ARCH] + CFLAGS)
+def _obj_digest(src):
+    return _digest([os.path.join(CSRC, src)] + _headers(src), [HIPCC, ARCH] + CFLAGS)
 
 
-def _lib_digest(hdr):
-    return hashlib.sha256("".join(_obj_digest(s, hdr) for s in SOURCES).encode()).hexdigest()
+def _lib_digest():
+    return hashlib.sha256("".join(_obj_digest(s) for s in SOURCES).encode()).hexdigest()
 
 
 def up_to_date():
     """True when every object and the library match the current sources, headers and flags."""
-    hdr = _headers()
-    if any(_stale(_obj(s), _obj_digest(s, hdr)) for s in SOURCES):
+    if any(_stale(_obj(s), _obj_digest(s)) for s in SOURCES):
         return False
-    return not _stale(LIB, _lib_digest(hdr))
+    return not _stale(LIB, _lib_digest())
 
 
 def _compile(src, verbose):
@@ -122,7 +138,7 @@ def _compile(src, verbose):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, obj)
-    _write_stamp(obj, _obj_digest(src, _headers()))
+    _write_stamp(obj, _obj_digest(src))
 
 
 def build(force=False, verbose=False):
@@ -130,9 +146,7 @@ def build(force=False, verbose=False):
     if not force and up_to_date():
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)
-    hdr = _headers()
-    hdr_sorted = sorted(hdr)
-    todo = [s for s in SOURCES if force or _stale(_obj(s), _obj_digest(s, hdr_sorted))]
+    todo = [s for s in SOURCES if force or _stale(_obj(s), _obj_digest(s))]
     with ThreadPoolExecutor(max(1, min(len(todo), int(os.environ.get("MAX_JOBS", "8"))))) as ex:
         list(ex.map(lambda s: _compile(s, verbose), todo))
     tmp = LIB + ".tmp"
@@ -141,7 +155,7 @@ def build(force=False, verbose=False):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
-    _write_stamp(LIB, _lib_digest(hdr_sorted))
+    _write_stamp(LIB, _lib_digest())
     return LIB
 
 

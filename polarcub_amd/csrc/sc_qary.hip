@@ -81,12 +81,17 @@ QGeom q_geom(int q, int n) {
     if (g_qregs > 0) c.S = (q <= 4 || g_qregs <= 4) ? g_qregs : 4;
     while (c.G > 1 && (1 << n) < 2 * c.S * c.G) c.G >>= 1;
     while (c.S > 1 && (1 << n) < 2 * c.S * c.G) c.S >>= 1;
+    // G = 8, 16 are instantiated for some (q, S) only: otherwise four lanes
+    if (c.G > 4 && !qary_kernel(q, c.S, c.G)) {
+        c.G = 4;
+        while (c.G > 1 && (1 << n) < 2 * c.S * c.G) c.G >>= 1;
+    }
     return c;
 }
 
 QKern qkernel(int q, int n, int* waves = nullptr) {
     const QGeom c = q_geom(q, n);
-    if (waves) *waves = qary_waves(q, c.S);
+    if (waves) *waves = qary_waves(q, c.S, c.G);
     return qary_kernel(q, c.S, c.G);
 }
 
@@ -181,9 +186,10 @@ extern "C" int pcub_polar_encode_qary(const uint8_t* info, int64_t B, int32_t lo
 }
 
 // Tuning hook (not part of the stable ABI): lanes per codeword of the q-ary
-// decode kernel (1, 2 or 4; reduced for short codes).  Returns the previous value.
+// decode kernel (1, 2, 4, 8 or 16; reduced for short codes, 8 and 16 where instantiated).
+// Returns the previous value.
 extern "C" int pcub_sc_set_qary_lanes(int G) {
-    if (G != 1 && G != 2 && G != 4) return PCUB_EINVAL;
+    if (G != 1 && G != 2 && G != 4 && G != 8 && G != 16) return PCUB_EINVAL;
     const int old = g_qlanes;
     g_qlanes = G;
     return old;

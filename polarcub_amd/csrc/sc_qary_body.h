@@ -181,12 +181,12 @@ struct QInfo {
     int w;     // next information row
     int j;     // lane of the codeword
     int gm;    // G - 1
-    uint32_t fm;  // frozen bits of the current register subtree's real u range
+    uint64_t fm;  // frozen bits of the current register subtree's real u range
     PCUB_HD void put(int u) {
         if (store && (w & gm) == j) info[(long long)w * B + cw] = (uint8_t)u;
         ++w;
     }
-    PCUB_HD bool frozen(int ub) const { return (fm >> ub) & 1u; }
+    PCUB_HD bool frozen(int ub) const { return (fm >> ub) & 1ull; }
 };
 
 // Exchange of a whole q-vector with lane ^ MASK.
@@ -386,15 +386,18 @@ PCUB_HD void q_final_dispatch(const QPass& P, QV<Q>* v, bool gop, bool root) {
 }
 
 // S = register positions per lane (a power of two), G lanes per codeword
-// (lane j of them, `lane` = wave lane id); requires N >= 2*S*G and S*G <= 32.
+// (lane j of them, `lane` = wave lane id); requires N >= 2*S*G and S*G <= 64.
+// G = 8, 16 hold one or two more tree levels per codeword on chip than G = 4 (one
+// stored stage level fewer each) at the price of duplicated work in the cross-lane
+// leaf levels (both lanes of an exchanging pair evaluate the same transform).
 template <int Q, int S, int G = 1, int U = 1>
 PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store, int j = 0, int lane = 0) {
     constexpr int s = (S == 1) ? 0 : (S == 2) ? 1 : (S == 4) ? 2 : (S == 8) ? 3 : 4;
-    constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : 2;
+    constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : (G == 4) ? 2 : (G == 8) ? 3 : 4;
     constexpr int SU = S * G;  // real u positions per register subtree
     constexpr int QP = (Q + 1) / 2;
-    static_assert(G == 1 || G == 2 || G == 4, "lanes per codeword");
-    static_assert(SU <= 32, "a register subtree's frozen bits fit one word");
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per codeword");
+    static_assert(SU <= 64, "a register subtree's frozen bits fit one 64-bit word");
     const int nv = A.n - g;
     const int Nv = 1 << nv;
     const long long ns = A.nslots;
@@ -448,7 +451,8 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
             else if (F == 2) q_final_dispatch<Q, S, 2>(P, v, gop, a == 0);
             else q_final_dispatch<Q, S, 1>(P, v, gop, a == 0);
             const int us = k * SU;
-            qi.fm = (A.fwords[us >> 5] >> (us & 31));
+            if constexpr (SU == 64) qi.fm = (uint64_t)A.fwords[us >> 5] | ((uint64_t)A.fwords[(us >> 5) + 1] << 32);
+            else qi.fm = (uint64_t)(A.fwords[us >> 5] >> (us & 31));
             QSub<Q, S, G>::run(v, y, 0, qi, lane);
         } else {
 #pragma unroll

@@ -18,9 +18,12 @@ constexpr int kQaryBlock = 256;
 // level (and q >= 6 vectors in the transforms) need two waves' worth of registers at
 // 32; up to 16 the kernel runs at four (the fastest q = 4 geometry, S = 4, G = 4:
 // 73.4M cw/s at 4 waves vs 71.0M at 3, profiles/r2/qary_*)
-constexpr int qary_waves(int q, int S) { return (q * S >= 32 || q >= 6) ? 2 : (q * S <= 16 ? 4 : 3); }
+// (G >= 8 with q * S = 32: three, the cross-lane leaves keep fewer vectors live)
+constexpr int qary_waves(int q, int S, int G = 4) {
+    return (G >= 8 && q * S == 32 && q < 6) ? 3 : (q * S >= 32 || q >= 6) ? 2 : (q * S <= 16 ? 4 : 3);
+}
 
-template <int Q, int S, int G, int W = qary_waves(Q, S), int U = 1>
+template <int Q, int S, int G, int W = qary_waves(Q, S, G), int U = 1>
 __global__ __launch_bounds__(kQaryBlock, W) void k_sc_qary(QArgs A) {
     constexpr int CWB = kQaryBlock / G;  // codewords per tile
     const long long slot = (long long)blockIdx.x * kQaryBlock + threadIdx.x;

@@ -3,6 +3,20 @@
 
 namespace pcub {
 
-QKern qary_kernel_q4(int S, int G) { return qary_kernel_geom<4, 8>(S, G); }
+// G = 8, 16 (one or two stored stage levels fewer, q-ary DESIGN 3.4) for the C4 alphabet
+QKern qary_kernel_q4(int S, int G) {
+    if (G == 8) {
+        if (S == 8) return k_sc_qary<4, 8, 8>;
+        if (S == 4) return k_sc_qary<4, 4, 8>;
+        if (S == 2) return k_sc_qary<4, 2, 8>;
+        return nullptr;
+    }
+    if (G == 16) {
+        if (S == 4) return k_sc_qary<4, 4, 16>;
+        if (S == 2) return k_sc_qary<4, 2, 16>;
+        return nullptr;
+    }
+    return qary_kernel_geom<4, 8>(S, G);
+}
 
 }  // namespace pcub

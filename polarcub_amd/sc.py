@@ -126,11 +126,11 @@ def set_max_blocks_per_cu(b):
 
 
 def set_qary_lanes(g):
-    """Lanes per codeword of the q-ary decode kernel (1, 2 or 4; reduced for short
-    codes).  Returns the previous setting."""
+    """Lanes per codeword of the q-ary decode kernel (1, 2, 4, 8 or 16; reduced for
+    short codes; 8 and 16 only where instantiated, else 4).  Returns the previous setting."""
     old = int(_lib.lib().pcub_sc_set_qary_lanes(int(g)))
     if old < 0:
-        raise ValueError("q-ary lanes per codeword must be 1, 2 or 4")
+        raise ValueError("q-ary lanes per codeword must be 1, 2, 4, 8 or 16")
     return old
 
 

@@ -7,7 +7,7 @@ from tests.conftest import load_golden
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-LANES = [1, 2, 4]  # lanes per codeword of the q-ary kernel
+LANES = [1, 2, 4, 8, 16]  # lanes per codeword of the q-ary kernel (8, 16: q = 4 only, else 4)
 
 
 @pytest.fixture(params=LANES)

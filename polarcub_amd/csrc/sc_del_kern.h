@@ -310,19 +310,46 @@ struct DelNode {
         } else {
             constexpr int H = LEN / 2;
             constexpr int d = (L / H == 2) ? 1 : (L / H == 4) ? 2 : (L / H == 8) ? 3 : 4;  // child depth
+            // minus then plus child through ONE call site, so the inlined subtree (and its
+            // private-memory trellises) exists once
             Trel<H, Cap::V, Cap::E(d)> c;
-            trellis_transform<LEN>(t, c, nullptr);
-            trellis_normalize<H>(c);
-            const uint32_t ym = DelNode<L, T, H, EXP, OC>::run(c, cx);
-            trellis_transform<LEN>(t, c, &ym);
-            trellis_normalize<H>(c);
-            const uint32_t yp = DelNode<L, T, H, EXP, OC>::run(c, cx);
+            uint32_t y[2];
+#pragma unroll 1
+            for (int half = 0; half < 2; ++half) {
+                trellis_transform<LEN>(t, c, half ? &y[0] : nullptr);
+                trellis_normalize<H>(c);
+                y[half] = DelNode<L, T, H, EXP, OC>::run(c, cx);
+            }
+            const uint32_t ym = y[0], yp = y[1];
             uint32_t x = 0;  // x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h]
 #pragma unroll
             for (int h = 0; h < H; ++h)
                 x |= ((((ym ^ yp) >> h) & 1u) << (2 * h)) | (((yp >> h) & 1u) << (2 * h + 1));
             return x;
         }
+    }
+};
+
+// The top trellis level for n0 >= 3 without guard-band ones: the base trellis is implicit
+// (BaseT, trellis_body.h), only its depth-1 children are materialised.
+template <int L, int T, bool EXP>
+struct DelBase {
+    __device__ static uint32_t run(const BaseT<L>& b, DelCtx<T, EXP>& cx) {
+        using Cap = DelCap<L, 0>;
+        constexpr int H = L / 2;
+        Trel<H, Cap::V, Cap::E(1)> c;
+        uint32_t y[2];
+#pragma unroll 1
+        for (int half = 0; half < 2; ++half) {
+            trellis_transform_base<L>(b, c, half ? &y[0] : nullptr);
+            trellis_normalize<H>(c);
+            y[half] = DelNode<L, T, H, EXP, 0>::run(c, cx);
+        }
+        const uint32_t ym = y[0], yp = y[1];
+        uint32_t x = 0;  // x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h]
+#pragma unroll
+        for (int h = 0; h < H; ++h) x |= ((((ym ^ yp) >> h) & 1u) << (2 * h)) | (((yp >> h) & 1u) << (2 * h + 1));
+        return x;
     }
 };
 
@@ -431,6 +458,8 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
         b.pins = 0.5 * (1.0 - A.pd);
         b.pdel = 0.5 * A.pd;
         x = del_n02(b, cx);
+    } else if constexpr (N0 >= 3 && OC == 0) {
+        x = DelBase<L, T, EXP>::run(base_segment<L>(bit, s, m, A.pd), cx);
     } else {
         Trel<L, Cap::V, Cap::E0> base;
         trellis_build<L>(base, bit, s, m, A.pd, A.op);

@@ -32,6 +32,8 @@
 // a depth-d trellis spans 2^d base layers, so it advances vpos by 0 .. 2^d: at most
 // 2V(2^d + 1) edges (one per from-vertex, advance, label), and never more than 2V^2.
 #pragma once
+#include <type_traits>
+
 #include "sc_common.h"
 
 namespace pcub {
@@ -44,6 +46,9 @@ PCUB_HD int ek_lbl(uint32_t k) { return (int)(k & 1u); }
 
 template <int LEN, int V, int E>
 struct Trel {
+    // edge indices and counts in the narrowest type that holds E (private memory is the
+    // deletion kernel's working set: every byte here is per trellis lane)
+    using EI = typename std::conditional<(E <= 127), int8_t, int16_t>::type;
     // direct-mapped lookups (validated on use, so they are never cleared): vertex index of a
     // vpos per layer, edge index of (from vertex, to vertex, label) per edge layer.  Without
     // them every addToEdgeProb is a linear search of the layer's edges, a chain of dependent
@@ -54,18 +59,18 @@ struct Trel {
     int16_t vp[LEN + 1][V]; // vpos in insertion order
     double pr0[V];          // vertex probabilities of layer 0 (insertion order)
     double prL[V];          // ... and of layer LEN
-    int16_t ne[LEN];        // edges per edge layer
+    EI ne[LEN];             // edges per edge layer
     uint32_t key[LEN][E];   // creation order
     double p[LEN][E];
     int8_t vidx[LEN + 1][VPM];
-    int16_t lut[LEN][V][V][2];
+    EI lut[LEN][V][V][2];
     // per edge: from / to vertex index; after index(): the edges of each layer grouped by
     // from-vertex and by to-vertex, each group in creation order (a stable counting sort), so
     // "vertices in order, then that vertex's edges in creation order" -- the reference's
     // iteration -- touches only those edges
     int8_t efv[LEN][E], etv[LEN][E];
-    int16_t byfrom[LEN][E], byto[LEN][E];
-    int16_t fstart[LEN][V + 1], tstart[LEN][V + 1];
+    EI byfrom[LEN][E], byto[LEN][E];
+    EI fstart[LEN][V + 1], tstart[LEN][V + 1];
 
     PCUB_HD void clear() {
         for (int l = 0; l <= LEN; ++l) nv[l] = 0;
@@ -112,8 +117,8 @@ struct Trel {
         p[l][c] = 0.0 + prob;
         efv[l][c] = (int8_t)ui;
         etv[l][c] = (int8_t)vi;
-        lut[l][ui][vi][x] = (int16_t)c;
-        ne[l] = (int16_t)(c + 1);
+        lut[l][ui][vi][x] = (EI)c;
+        ne[l] = (EI)(c + 1);
     }
     // group every edge layer by from-vertex and by to-vertex (structure only: p may change later)
     PCUB_HD void index() {
@@ -128,14 +133,14 @@ struct Trel {
                 fstart[l][v + 1] += fstart[l][v];
                 tstart[l][v + 1] += tstart[l][v];
             }
-            int16_t fp[V], tp[V];
+            EI fp[V], tp[V];
             for (int v = 0; v < V; ++v) {
                 fp[v] = fstart[l][v];
                 tp[v] = tstart[l][v];
             }
             for (int e = 0; e < n; ++e) {
-                byfrom[l][fp[efv[l][e]]++] = (int16_t)e;
-                byto[l][tp[etv[l][e]]++] = (int16_t)e;
+                byfrom[l][fp[efv[l][e]]++] = (EI)e;
+                byto[l][tp[etv[l][e]]++] = (EI)e;
             }
         }
     }
@@ -217,6 +222,112 @@ PCUB_HD void trellis_transform(const P& pt, C& ct, const uint32_t* dec) {
                         ct.add(j, ek_from(ka), ek_to(kb), ml, prob);
                     } else if (ml == dj) {
                         ct.add(j, ek_from(ka), ek_to(kb), ek_lbl(kb), prob);
+                    }
+                }
+            }
+        }
+    }
+    ct.index();
+}
+
+// The base trellis of one segment without guard-band ones, never stored (trellis_n02.h's
+// Base02 for any length L): buildTrellis_uniformInput_deletion (BinaryTrellis.py:384-436)
+// walks the layers in order and, inside layer l, the from-positions vp in [lo(l), hi(l)]
+// ascending, creating the insertion edge vp -> vp+1 (label y[vp]) and then the deletion
+// edges vp -> vp (labels 0, 1).  So a vertex's out-edges in dict order are [insertion,
+// deletion 0, deletion 1], its in-edges [insertion from vp-1, deletion 0, deletion 1 from
+// vp], and the vertices of a middle layer are inserted in the order the previous layer's
+// edges first reach them.  Its only layer-0 / layer-L vertices are vpos 0 and m (vertex
+// probability 1.0), and edges exist only when m <= L.
+template <int L>
+struct BaseT {
+    static constexpr int V = L / 2 + 1;  // vertices per layer, at most (DelCap<L, 0>::V)
+    int m;
+    int d;        // deletions: L - m
+    uint32_t y;   // received bits of the segment (m <= L)
+    double pins;  // 0.5 (1 - pd)
+    double pdel;  // 0.5 pd
+    PCUB_HD int lo(int l) const { return l - d > 0 ? l - d : 0; }
+    PCUB_HD int hi(int l) const { return l < m ? l : m; }
+    PCUB_HD bool from_ok(int l, int vp) const { return vp >= lo(l) && vp <= hi(l); }
+    // edge leaving (l, vp) of kind 0 = insertion, 1 = deletion 0, 2 = deletion 1
+    PCUB_HD bool out_edge(int l, int vp, int kind, int& to, int& lbl, double& p) const {
+        if (!from_ok(l, vp)) return false;
+        if (kind == 0) {
+            if (vp >= m) return false;
+            to = vp + 1;
+            lbl = (int)((y >> vp) & 1u);
+            p = pins;
+            return true;
+        }
+        if (l + 1 - d > vp) return false;
+        to = vp;
+        lbl = kind - 1;
+        p = (kind == 1 && !(vp > 0 && vp < m)) ? 0.5 : pdel;
+        return true;
+    }
+    // Vertices of middle layer l (1 <= l < L) that have in-edges, in insertion order.  The
+    // edges of layer l-1 reach, in creation order: lo+1 (insertion from lo), lo (deletion
+    // from lo), then vp+1 for every later from-position vp (its deletion target vp was
+    // already reached by the insertion from vp-1), with lo = lo(l-1).
+    PCUB_HD int nreached(int l) const {
+        const int a = lo(l - 1);
+        if (a > hi(l - 1)) return 0;  // m > L: no edges
+        const int last = hi(l - 1) < m - 1 ? hi(l - 1) : m - 1;  // last from-position with an insertion
+        return (a < m ? 1 : 0) + (l - d <= a ? 1 : 0) + (last > a ? last - a : 0);
+    }
+    PCUB_HD int reached(int l, int i) const {
+        const int a = lo(l - 1);
+        const int c0 = a < m ? 1 : 0;
+        const int c1 = l - d <= a ? 1 : 0;
+        if (i < c0) return a + 1;
+        if (i < c0 + c1) return a;
+        return a + 2 + (i - c0 - c1);
+    }
+};
+
+template <int L, class BitF>
+PCUB_HD BaseT<L> base_segment(const BitF& bit, int s, int m, double pd) {
+    BaseT<L> b;
+    b.m = m;
+    b.d = L - m;
+    b.y = 0;
+    if (m <= L)
+        for (int i = 0; i < m; ++i) b.y |= (uint32_t)(bit(s + i) & 1) << i;
+    b.pins = 0.5 * (1.0 - pd);
+    b.pdel = 0.5 * pd;
+    return b;
+}
+
+// trellis_transform with the base trellis as the parent (same iteration: middle vertices
+// in insertion order, in-edges x out-edges in creation order, products pa * pb).
+template <int L, class C>
+PCUB_HD void trellis_transform_base(const BaseT<L>& b, C& ct, const uint32_t* dec) {
+    constexpr int H = L / 2;
+    ct.clear();
+    ct.set_prob(0, 0, 1.0);
+    ct.set_prob(H, b.m, 1.0);
+    for (int j = 0; j < H; ++j) {
+        const int mid = 2 * j + 1;
+        const int dj = dec ? (int)((*dec >> j) & 1u) : 0;
+        const int nw = b.nreached(mid);
+        for (int wi = 0; wi < nw; ++wi) {
+            const int w = b.reached(mid, wi);
+            for (int a = 0; a < 3; ++a) {
+                const int u = a == 0 ? w - 1 : w;
+                int tu, lu;
+                double pu;
+                if (!b.out_edge(mid - 1, u, a, tu, lu, pu) || tu != w) continue;
+                for (int o = 0; o < 3; ++o) {
+                    int tv, lv;
+                    double pv;
+                    if (!b.out_edge(mid, w, o, tv, lv, pv)) continue;
+                    const double prob = pu * pv;
+                    const int ml = lu ^ lv;
+                    if (!dec) {
+                        ct.add(j, u, tv, ml, prob);
+                    } else if (ml == dj) {
+                        ct.add(j, u, tv, lv, prob);
                     }
                 }
             }

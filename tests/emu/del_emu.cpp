@@ -58,8 +58,57 @@ constexpr int depth_of(int len) {
     return (L / len == 1) ? 0 : (L / len == 2) ? 1 : (L / len == 4) ? 2 : (L / len == 8) ? 3 : 4;
 }
 
+// the kernel's top level for n0 >= 3 without ones: children of the implicit base trellis
+// (BaseT), which must equal the children of the stored one field by field
+std::vector<BaseT<16>> g_base;  // per trellis, the segment (m, bits) as BaseT<L> sees it
+bool g_use_base = false;
+long long g_base_checks = 0;
+
+template <class A, class B>
+void same_trellis(const A& x, const B& y, int len) {
+    for (int l = 0; l <= len; ++l) {
+        if (x.nv[l] != y.nv[l]) throw 4;
+        for (int i = 0; i < x.nv[l]; ++i)
+            if (x.vp[l][i] != y.vp[l][i]) throw 4;
+    }
+    for (int i = 0; i < x.nv[0]; ++i)
+        if (as_bits(x.pr0[i]) != as_bits(y.pr0[i])) throw 4;
+    for (int i = 0; i < x.nv[len]; ++i)
+        if (as_bits(x.prL[i]) != as_bits(y.prL[i])) throw 4;
+    for (int l = 0; l < len; ++l) {
+        if (x.ne[l] != y.ne[l]) throw 4;
+        for (int e = 0; e < x.ne[l]; ++e)
+            if (x.key[l][e] != y.key[l][e] || as_bits(x.p[l][e]) != as_bits(y.p[l][e])) throw 4;
+    }
+}
+
+template <int L>
+BaseT<L> base_of(int t) {
+    BaseT<L> b;
+    b.m = g_base[t].m;
+    b.d = L - b.m;
+    b.y = g_base[t].y;
+    b.pins = g_base[t].pins;
+    b.pdel = g_base[t].pdel;
+    return b;
+}
+
 template <int L, int LEN, int OC>
 struct Node {
+    template <class PT, class CT>
+    static void child(const std::vector<PT>& ts, size_t t, CT& c, const uint32_t* dec) {
+        trellis_transform<LEN>(ts[t], c, dec);
+        if constexpr (LEN == L && OC == 0 && L >= 8) {
+            if (g_use_base) {
+                Trel<LEN / 2, Cap<L, OC>::V, Cap<L, OC>::E(depth_of<L>(LEN / 2))> cb;
+                trellis_transform_base<L>(base_of<L>((int)t), cb, dec);
+                same_trellis(cb, c, LEN / 2);
+                ++g_base_checks;
+                trellis_transform_base<L>(base_of<L>((int)t), c, dec);  // the kernel's child
+            }
+        }
+    }
+
     template <class PT>
     static std::vector<uint32_t> run(const std::vector<PT>& ts, Ctx& cx, int ones) {
         const size_t T = ts.size();
@@ -92,12 +141,12 @@ struct Node {
             using CT = Trel<H, Cap<L, OC>::V, Cap<L, OC>::E(depth_of<L>(H))>;
             std::vector<CT> cs(T);
             for (size_t t = 0; t < T; ++t) {
-                trellis_transform<LEN>(ts[t], cs[t], nullptr);
+                child(ts, t, cs[t], nullptr);
                 trellis_normalize<H>(cs[t]);
             }
             const std::vector<uint32_t> ym = Node<L, H, OC>::run(cs, cx, ones);
             for (size_t t = 0; t < T; ++t) {
-                trellis_transform<LEN>(ts[t], cs[t], &ym[t]);
+                child(ts, t, cs[t], &ym[t]);
                 trellis_normalize<H>(cs[t]);
             }
             const std::vector<uint32_t> yp = Node<L, H, OC>::run(cs, cx, ones);
@@ -183,10 +232,16 @@ void decode_one_oc(const uint8_t* w, int len, int n, double pd, int ones, Ctx& c
     auto bit = [w](int i) { return (int)w[i]; };
     const OnesProbs op = ones_probs(ones, pd);
     std::vector<Trel<L, Cap<L, OC>::V, Cap<L, OC>::E0>> base(T);
+    g_base.assign(T, BaseT<16>{});
     for (int t = 0; t < T; ++t) {
         int s, m;
         segment_of(bit, len, tb, t, s, m);
         trellis_build<L>(base[t], bit, s, m, pd, op);
+        const BaseT<L> b = base_segment<L>(bit, s, m, pd);
+        g_base[t].m = b.m;
+        g_base[t].y = b.y;
+        g_base[t].pins = b.pins;
+        g_base[t].pdel = b.pdel;
     }
     std::vector<uint32_t> x;
     if constexpr (N0 == 2 && OC == 0) {
@@ -231,8 +286,9 @@ extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, lon
                 case 4: decode_one<4>(w, len, n, pd, ones, cx, xh); break;
                 default: return -1;
             }
-        } catch (int) {
-            return -3;  // trellis_collapse disagrees with the materialised child's marginal
+        } catch (int e) {
+            return e == 4 ? -4    // the implicit base's child differs from the stored base's
+                          : -3;   // trellis_collapse disagrees with the materialised child's marginal
         }
         if ((int)cx.info.size() != K) return -2;
         for (int i = 0; i < K; ++i)
@@ -244,6 +300,10 @@ extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, lon
 }
 
 extern "C" void emu_set_n02(int on) { use_n02 = on != 0; }
+
+// n0 >= 3 without ones: the top level from the implicit base trellis (checked against the stored one)
+extern "C" void emu_set_base(int on) { g_use_base = on != 0; }
+extern "C" long long emu_base_checks() { return g_base_checks; }
 
 // segment_of on bytes vs segment_of_packed on the packed word (the kernel's parse), for
 // random words with long zero runs (guard bands) and every trellis of 1..6 levels.

@@ -68,6 +68,17 @@ def test_edge_golden(idx, n02):
     assert np.array_equal(xhat, c["xhat"])
 
 
+@pytest.mark.parametrize("idx", range(11))
+def test_edge_golden_implicit_base(idx, implicit_base):
+    c = deletion_edge_cases()[idx]
+    n, n0, ones = (int(v) for v in c["shape"])
+    if n0 < 3 or ones != 0:
+        pytest.skip("the implicit base trellis is the n0 >= 3 path without guard-band ones")
+    info, xhat = run(c["rx"], c["rx_len"], n, n0, float(c["pd"][0]), c["frozen"], c["fval"], ones)
+    assert np.array_equal(info, c["info"])
+    assert np.array_equal(xhat, c["xhat"])
+
+
 @pytest.mark.parametrize("n", [3, 5, 8])
 def test_n02_random_vs_oracle(n):
     """Register-resident n0 = 2 path on random channel outputs and adversarial words."""
@@ -107,9 +118,19 @@ def test_packed_segment_parse_matches_byte_parse():
     assert L.emu_check_segments(ctypes.c_uint64(12345), 3000) == 0
 
 
+@pytest.fixture(params=[False, True], ids=["stored-base", "implicit-base"])
+def implicit_base(request):
+    """n0 >= 3 without guard-band ones: the kernel never stores the base trellis (BaseT,
+    trellis_body.h); the emulator then builds the top level's children from it and checks
+    each one against the stored base's child, field by field."""
+    emu().emu_set_base(int(request.param))
+    yield request.param
+    emu().emu_set_base(0)
+
+
 @pytest.mark.parametrize("n0,n,ones", [(3, 10, 0), (3, 11, 0), (4, 12, 0), (4, 6, 0), (2, 5, 1), (1, 4, 2),
-                                       (3, 6, 3), (4, 6, 2), (2, 9, 0)])
-def test_wide_shapes_vs_oracle(n0, n, ones):
+                                       (3, 6, 3), (4, 6, 2), (2, 9, 0), (3, 7, 0), (4, 8, 0)])
+def test_wide_shapes_vs_oracle(n0, n, ones, implicit_base):
     """Shapes the widened kernel adds: more than 64 trellises (main_deletion.py's n0 = n // 3
     at n = 10..12), 16-input trellises and guard-band ones (capacities, vertex probabilities,
     the materialised collapse), against the oracle."""
@@ -132,7 +153,12 @@ def test_wide_shapes_vs_oracle(n0, n, ones):
     rx = np.zeros((len(words), W), np.uint8)
     for i, w in enumerate(words):
         rx[i, :len(w)] = w
+    L = emu()
+    L.emu_base_checks.restype = ctypes.c_longlong
+    checks0 = L.emu_base_checks()
     info, xhat = run(rx, np.array([len(w) for w in words], np.int32), n, n0, pd, frozen, fval, ones)
+    if implicit_base and n0 >= 3 and ones == 0:
+        assert L.emu_base_checks() > checks0
     for i, w in enumerate(words):
         xr, ir = tro.decode_deletion(w, n, n0, pd, frozen, fval, ones=ones)
         assert list(info[i]) == ir and list(xhat[i]) == xr, i

@@ -66,7 +66,7 @@ struct DelArgs {
 // leaf[u * B] -- the xy marginals the genie reads (BinaryPolarEncoderDecoder.py:268-273).
 template <int M, int UBASE>
 struct XSubE {
-    __device__ static uint32_t run(double v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane, double* leaf,
+    __device__ __forceinline__ static uint32_t run(double v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane, double* leaf,
                                    long long B, bool store) {
         const double w = xor_shfl_c<M / 2>(v);
         const bool lo = (lane & (M / 2)) == 0;
@@ -296,7 +296,7 @@ __device__ __forceinline__ void del_collapse(const PT& t, const uint32_t* dec, i
 template <int L, int T, int LEN, bool EXP, int OC>
 struct DelNode {
     template <class PT>
-    __device__ static uint32_t run(const PT& t, DelCtx<T, EXP>& cx) {
+    __device__ __forceinline__ static uint32_t run(const PT& t, DelCtx<T, EXP>& cx) {
         using Cap = DelCap<L, OC>;
         if constexpr (LEN == 2) {
             // children are length-1 trellises collapsed to memoryless rows
@@ -310,17 +310,13 @@ struct DelNode {
         } else {
             constexpr int H = LEN / 2;
             constexpr int d = (L / H == 2) ? 1 : (L / H == 4) ? 2 : (L / H == 8) ? 3 : 4;  // child depth
-            // minus then plus child through ONE call site, so the inlined subtree (and its
-            // private-memory trellises) exists once
             Trel<H, Cap::V, Cap::E(d)> c;
-            uint32_t y[2];
-#pragma unroll 1
-            for (int half = 0; half < 2; ++half) {
-                trellis_transform<LEN>(t, c, half ? &y[0] : nullptr);
-                trellis_normalize<H>(c);
-                y[half] = DelNode<L, T, H, EXP, OC>::run(c, cx);
-            }
-            const uint32_t ym = y[0], yp = y[1];
+            trellis_transform<LEN>(t, c, nullptr);
+            trellis_normalize<H>(c);
+            const uint32_t ym = DelNode<L, T, H, EXP, OC>::run(c, cx);
+            trellis_transform<LEN>(t, c, &ym);
+            trellis_normalize<H>(c);
+            const uint32_t yp = DelNode<L, T, H, EXP, OC>::run(c, cx);
             uint32_t x = 0;  // x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h]
 #pragma unroll
             for (int h = 0; h < H; ++h)
@@ -334,7 +330,7 @@ struct DelNode {
 // (BaseT, trellis_body.h), only its depth-1 children are materialised.
 template <int L, int T, bool EXP>
 struct DelBase {
-    __device__ static uint32_t run(const BaseT<L>& b, DelCtx<T, EXP>& cx) {
+    __device__ __forceinline__ static uint32_t run(const BaseT<L>& b, DelCtx<T, EXP>& cx) {
         using Cap = DelCap<L, 0>;
         constexpr int H = L / 2;
         Trel<H, Cap::V, Cap::E(1)> c;

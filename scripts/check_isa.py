@@ -9,6 +9,12 @@ every device function must either be inlined or free of s_setpc_b64 s[30:31] oth
 its final return.
 
     python scripts/check_isa.py [path/to/libpolarcub_hip.so]
+Second rule: cross-lane operations (ds_bpermute / ds_permute / ds_swizzle, DPP moves) live
+in kernels only, or in an allowlisted leaf function called under a full wave.  Out-of-line
+deletion node functions with lane exchanges gave batch-dependent wrong results on the GPU
+(round 2: 32-trellis shapes, the host emulation clean under ASan/UBSan); they are
+force-inlined, and this rule keeps them so.
+
 Exit status 1 lists the offending functions.
 """
 import os
@@ -61,6 +67,12 @@ def device_disasm(lib):
     return "\n".join(texts)
 
 
+# device functions allowed to exchange lanes: called by wave 0 of the deletion kernel with all
+# lanes active (the T > 64 window decoder, kept out of line for the branch range above)
+CROSS_LANE_OK = ("del_window",)
+CROSS_LANE = re.compile(r"ds_bpermute|ds_permute|ds_swizzle|quad_perm|row_ror|row_shl|row_shr|row_mirror|row_bcast|wave_")
+
+
 def main():
     lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "polarcub_amd", "lib", "libpolarcub_hip.so")
     text = device_disasm(lib)
@@ -81,9 +93,12 @@ def main():
                 if re.search(r"s_getpc_b64 s\[30:31\]|s_add_u32 s30|s_addc_u32 s31|s_sub_u32 s30", prev):
                     n += 1
         if n:
-            bad.append((name, n))
-    for name, n in bad:
-        print("long branch through the return address in device function %s (%d long branch(es) via s[30:31])" % (name, n))
+            bad.append((name, n, "long branch through the return address (%d long branch(es) via s[30:31])" % n))
+        x = len(CROSS_LANE.findall(body))
+        if x and not any(a in name for a in CROSS_LANE_OK):
+            bad.append((name, x, "cross-lane operations in an out-of-line device function (%d)" % x))
+    for name, n, what in bad:
+        print("%s in device function %s" % (what, name))
     print("%d function(s) checked, %d hazard(s)" % (len(re.findall(r"^[0-9a-f]+ <", text, re.M)), len(bad)))
     return 1 if bad else 0
 

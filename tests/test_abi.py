@@ -59,7 +59,9 @@ def test_oracle_and_emulator_build():
 def test_no_long_branch_through_the_return_address():
     """scripts/check_isa.py: no device function of the built code object computes a long
     branch into s[30:31] (LLVM's expansion clobbers the return address; seen as an illegal
-    memory access in a round-2 deletion callee)."""
+    memory access in a round-2 deletion callee), and no out-of-line device function other
+    than the allowlisted window decoder exchanges lanes (out-of-line deletion node functions
+    gave batch-dependent wrong results on the GPU)."""
     import subprocess
     import sys
     from polarcub_amd import build

@@ -42,15 +42,18 @@ KernFn variant_kernel(int v) {
     return bin_kernel_part3(v);
 }
 
-// {32, 4, 3, NT}: fastest at N=1024 on MI355X (profiles/r1/sweep_*.txt)
-constexpr int kDefaultVariant = 17;
+// {32, 4, 3, NT, re-encoded bits in LDS}: fastest at N=1024 and N=4096 on MI355X
+// (73.9 / 13.3 M cw/s vs 72.0 / 12.5 M for its global-bits twin 17, profiles/r2/ylds/);
+// past the LDS budget (N > 4096) pick_variant falls back to 17
+constexpr int kDefaultVariant = 24;
 int g_variant = kDefaultVariant;
 int g_max_blocks = 0;  // workgroups per CU cap (0 = as many as fit)
 constexpr size_t kLdsPerCu = 160 * 1024;
 
-// dynamic LDS for variant v: its stage level plus padding that caps residency at g_max_blocks
-size_t launch_lds(int v) {
-    size_t b = bin_lds_bytes(v);
+// dynamic LDS for variant v at code length 2^n: its stage level, its re-encoded bits, plus
+// padding that caps residency at g_max_blocks
+size_t launch_lds(int v, int n) {
+    size_t b = bin_lds_bytes(v) + bin_ylds_bytes(v, n);
     if (g_max_blocks > 0) {
         const size_t cap = kLdsPerCu / (size_t)g_max_blocks;
         if (cap > b) b = cap - 256;
@@ -93,18 +96,21 @@ int tree_depth(int n, int v) {
 }
 size_t ef_bytes(int n, int v) { return (((size_t)1 << tree_depth(n, v)) + 255) & ~(size_t)255; }
 
-// per-slot bytes: virtual levels 1..D-1 (Nv/2 - S pairs) + Nv local encoding bits
+// per-slot bytes: virtual levels 1..D-1 (Nv/2 - S pairs) + Nv local encoding bits (unless in LDS)
 size_t slot_bytes(int n, int v) {
     const size_t Nv = ((size_t)1 << n) / kVar[v].G;
-    return (Nv / 2 - kVar[v].S) * sizeof(double2) + (Nv / 32) * sizeof(uint32_t);
+    return (Nv / 2 - kVar[v].S) * sizeof(double2) + (kVar[v].Y ? 0 : (Nv / 32) * sizeof(uint32_t));
 }
 
-long long grid_for(long long B, int v) {
+long long grid_for(long long B, int v, int n) {
     const DevInfo d = dev_info();
     if (d.cus <= 0) return 0;
     const long long cwb = kBlock / kVar[v].G;
     const long long ntiles = (B + cwb - 1) / cwb;
     int occ = d.occ[v];
+    const size_t lds = launch_lds(v, n);
+    if (lds > 0 && (size_t)occ * lds > kLdsPerCu) occ = (int)(kLdsPerCu / lds);
+    if (occ < 1) occ = 1;
     if (g_max_blocks > 0 && g_max_blocks < occ) occ = g_max_blocks;
     long long g = (long long)d.cus * occ;
     return ntiles < g ? ntiles : g;
@@ -113,8 +119,11 @@ long long grid_for(long long B, int v) {
 // a variant needs at least one outer level (N >= 2*S*G) and whole-word x_hat
 // segments (N >= 32*G); otherwise fall back to the first variant of a
 // decreasing-subtree list that fits (v1 = {8, 1} fits every N >= 64).
+// A Y variant fits while its W workgroups' re-encoded bits fit the CU's LDS
+// (N <= 4096 at G = 4); beyond that its non-LDS twin takes over.
 bool fits(int v, int n) {
     const long long N = 1LL << n;
+    if (kVar[v].Y && (size_t)kVar[v].W * launch_lds(v, n) > kLdsPerCu) return false;
     return N >= 2LL * kVar[v].S * kVar[v].G && N >= 32LL * kVar[v].G;
 }
 int pick_variant(int n) {
@@ -155,7 +164,7 @@ extern "C" size_t pcub_sc_decode_bin_workspace(int64_t B, int32_t log2N) {
     if (B <= 0 || log2N < 0 || log2N > 24) return 0;
     if (log2N < 6) return 0;
     const int v = pick_variant(log2N);
-    const long long g = grid_for(B, v);
+    const long long g = grid_for(B, v, log2N);
     return ef_bytes(log2N, v) + (size_t)g * kBlock * slot_bytes(log2N, v);
 }
 
@@ -192,7 +201,7 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
         return (int)hipGetLastError();
     }
     const int v = pick_variant(log2N);
-    long long g = grid_for(B, v);
+    long long g = grid_for(B, v, log2N);
     if (g <= 0) return (int)hipErrorNoDevice;
     const size_t per_block = (size_t)kBlock * slot_bytes(log2N, v);
     if (!workspace) return PCUB_EINVAL;
@@ -209,7 +218,7 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
     A.ef = ef;
     A.nslots = nslots;
     A.scratch = (double2*)slots;
-    A.ybits = (uint32_t*)(slots + (size_t)nslots * (Nv / 2 - kVar[v].S) * sizeof(double2));
-    hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), launch_lds(v), st, A);
+    A.ybits = kVar[v].Y ? nullptr : (uint32_t*)(slots + (size_t)nslots * (Nv / 2 - kVar[v].S) * sizeof(double2));
+    hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), launch_lds(v, log2N), st, A);
     return (int)hipGetLastError();
 }

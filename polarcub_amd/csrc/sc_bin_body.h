@@ -267,6 +267,28 @@ PCUB_HD void stu(uint32_t* p, uint32_t v) {
 #endif
 }
 
+// Re-encoded bits (Y): a per-slot global buffer, or (YL) this thread's column of an LDS
+// array (word w at Y[w * kBinBlock]): the plus passes read them and every combine rewrites
+// them, so in LDS they never travel to L2/HBM.
+template <bool YL>
+PCUB_HD uint32_t ldy(const uint32_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (YL) return *(const __attribute__((address_space(3))) uint32_t*)p;
+#endif
+    return ldu(p);
+}
+
+template <bool YL>
+PCUB_HD void sty(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (YL) {
+        *(__attribute__((address_space(3))) uint32_t*)p = v;
+        return;
+    }
+#endif
+    stu(p, v);
+}
+
 // Root rows.  Local position t of lane j is real position p = j + G*t < N/2,
 // which pairs natural rows (2q, 2q+1) with q = bitrev_{n-1}(p).  The bits of j
 // and of G*t are disjoint, so q = bitrev_{n-1}(j) + bitrev_{nv-1}(t): the lane
@@ -300,7 +322,7 @@ PCUB_HD void sched_fence() {
 // minus transform; every later op is a minus transform (an SC chain descends
 // through minus children).  y receives levels a+1 .. a+F back to back
 // (2^(F-1), 2^(F-2), .., 1 entries; .x = column p, .y = column p+1).
-template <int F, bool FG, int R, int G, bool NS = false, bool GL = true>
+template <int F, bool FG, int R, int G, bool NS = false, bool GL = true, bool YL = false>
 PCUB_HD void colpair(const Chain& c, int p, int C, double2* y) {
     constexpr bool ROOT = R != 0;
     constexpr int H = 1 << (F - 1);
@@ -310,7 +332,7 @@ PCUB_HD void colpair(const Chain& c, int p, int C, double2* y) {
         uint32_t u0 = 0, u1 = 0;
         if (FG) {
             const int bp = c.ystart + P;  // even: bits bp, bp+1 share a word
-            const uint32_t w = ldu(c.Y + (long long)(bp >> 5) * c.ns) >> (bp & 31);
+            const uint32_t w = ldy<YL>(c.Y + (long long)(bp >> 5) * c.ns) >> (bp & 31);
             u0 = w & 1u;
             u1 = (w >> 1) & 1u;
         }
@@ -361,7 +383,7 @@ struct LevelMap {
 };
 
 // Non-final pass: levels a+1 .. a+F are all stored.
-template <int F, bool FG, int R, int G, bool NS>
+template <int F, bool FG, int R, int G, bool NS, bool YL>
 PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
     Lvl lv[F];
 #pragma unroll
@@ -370,7 +392,7 @@ PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
 #pragma unroll 1
     for (int p = 0; p < C; p += 2) {
         double2 y[(1 << F) - 1];
-        colpair<F, FG, R, G, NS>(c, p, C, y);
+        colpair<F, FG, R, G, NS, true, YL>(c, p, C, y);
         int off = 0;
 #pragma unroll
         for (int e = 1; e <= F; ++e) {
@@ -387,13 +409,13 @@ PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
 // passes (stored here, or read as c.src when F = 1), which lets it live in LDS
 // with static addressing.  (A three-level final pass from the root needs more
 // than the 168 VGPRs of three waves/SIMD with S = 32 and spills.)
-template <int S, int F, bool FG, int R, int G, bool NS, bool LL>
+template <int S, int F, bool FG, int R, int G, bool NS, bool LL, bool YL>
 PCUB_HD void chain_final(const Chain& c, const Lvl* lv, double* v) {
     static_assert(F == 1 || F == 2, "final pass fuses at most two levels");
 #pragma unroll
     for (int p = 0; p < S; p += 2) {
         double2 y[(1 << F) - 1];
-        colpair<F, FG, R, G, NS && F == 2, F == 2 || !LL>(c, p, S, y);
+        colpair<F, FG, R, G, NS && F == 2, F == 2 || !LL, YL>(c, p, S, y);
         if constexpr (F == 2) {
 #pragma unroll
             for (int m = 0; m < 2; ++m) st2<false, !LL>(lv[0].p + (long long)((p + m * S) >> 1) * lv[0].s, y[m]);
@@ -406,25 +428,25 @@ PCUB_HD void chain_final(const Chain& c, const Lvl* lv, double* v) {
 
 // root: 0 = compact source level, RR = root (1 plain, 2 non-temporal loads)
 // NS: non-temporal access to the upper stage levels (all but level D-1)
-template <int F, int G, int RR, bool NS>
+template <int F, int G, int RR, bool NS, bool YL>
 PCUB_HD void dispatch_pass(const Chain& c, int La, const LevelMap& lm, int a, bool fg, bool root) {
     if (root) {
-        if (fg) chain_pass<F, true, RR, G, NS>(c, La, lm, a);
-        else chain_pass<F, false, RR, G, NS>(c, La, lm, a);
+        if (fg) chain_pass<F, true, RR, G, NS, YL>(c, La, lm, a);
+        else chain_pass<F, false, RR, G, NS, YL>(c, La, lm, a);
     } else {
-        if (fg) chain_pass<F, true, 0, G, NS>(c, La, lm, a);
-        else chain_pass<F, false, 0, G, NS>(c, La, lm, a);
+        if (fg) chain_pass<F, true, 0, G, NS, YL>(c, La, lm, a);
+        else chain_pass<F, false, 0, G, NS, YL>(c, La, lm, a);
     }
 }
 
-template <int S, int F, int G, int RR, bool NS, bool LL>
+template <int S, int F, int G, int RR, bool NS, bool LL, bool YL>
 PCUB_HD void dispatch_final(const Chain& c, const Lvl* lv, double* v, bool fg, bool root) {
     if (root) {
-        if (fg) chain_final<S, F, true, RR, G, NS, LL>(c, lv, v);
-        else chain_final<S, F, false, RR, G, NS, LL>(c, lv, v);
+        if (fg) chain_final<S, F, true, RR, G, NS, LL, YL>(c, lv, v);
+        else chain_final<S, F, false, RR, G, NS, LL, YL>(c, lv, v);
     } else {
-        if (fg) chain_final<S, F, true, 0, G, NS, LL>(c, lv, v);
-        else chain_final<S, F, false, 0, G, NS, LL>(c, lv, v);
+        if (fg) chain_final<S, F, true, 0, G, NS, LL, YL>(c, lv, v);
+        else chain_final<S, F, false, 0, G, NS, LL, YL>(c, lv, v);
     }
 }
 
@@ -516,9 +538,10 @@ struct SubWin {
 };
 
 // NT: 0 = cached loads/stores, 1 = non-temporal input rows, 2 = also the upper stage levels
-template <int S, int G, bool LDS = false, int NT = 0>
+// YL: the re-encoded bits in LDS (ylds = this thread's column, word w at ylds[w * ystride])
+template <int S, int G, bool LDS = false, int NT = 0, bool YL = false>
 PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
-                             Lvl last = Lvl{nullptr, 0}) {
+                             Lvl last = Lvl{nullptr, 0}, uint32_t* ylds = nullptr, long long ystride = 0) {
     static_assert(S == 8 || S == 16 || S == 32, "register subtree must fit one Y word");
     static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per codeword");
     constexpr int s = (S == 8) ? 3 : (S == 16) ? 4 : 5;
@@ -537,7 +560,8 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     const long long B = A.B;
     const double2* in = A.xy + cw + 2 * (long long)bitrev((uint32_t)j, n - 1) * B;
     double2* scr = A.scratch + slot;
-    uint32_t* Y = A.ybits + slot;
+    uint32_t* Y = YL ? ylds : A.ybits + slot;
+    const long long ys = YL ? ystride : ns;  // Y word stride
 
     // stored levels 1 .. D-2 in the slot scratch; level D-1 there too, or in LDS (`last`)
     LevelMap lm;
@@ -557,7 +581,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     for (int k = 0; k < (1 << D); ++k) {
         in = launder(in);
         scr = launder(scr);
-        Y = launder(Y);
+        if constexpr (!YL) Y = launder(Y);
         lm.scr = scr;
         if constexpr (!LDS) lastlv = lm.get(D - 1);
         // The chain for subtree k: a plus transform at depth d0-1 (minus for k == 0)
@@ -574,7 +598,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         c.B = B;
         c.nv = nv;
         c.Y = Y;
-        c.ns = ns;
+        c.ns = ys;
         // frozen bits of real u range [k*SU, (k+1)*SU), in NW windows
         uint64_t fm[NW], fv[NW], ub[NW];
 #pragma unroll
@@ -600,9 +624,9 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
                 c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
                 c.ystart = (k >> (D - a)) << (nv - a);
                 const int La = Nv >> a;
-                if (F == 3) dispatch_pass<3, G, RR, NS>(c, La, lm, a, fg, a == 0);
-                else if (F == 2) dispatch_pass<2, G, RR, NS>(c, La, lm, a, fg, a == 0);
-                else dispatch_pass<1, G, RR, NS>(c, La, lm, a, fg, a == 0);
+                if (F == 3) dispatch_pass<3, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
+                else if (F == 2) dispatch_pass<2, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
+                else dispatch_pass<1, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
                 a += F;
                 T -= F;
                 fg = false;
@@ -616,9 +640,9 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
             c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
             c.ystart = (k >> (D - a)) << (nv - a);
             const int La = Nv >> a;
-            if (F == 3) dispatch_pass<3, G, RR, NS>(c, La, lm, a, fg, a == 0);
-            else if (F == 2) dispatch_pass<2, G, RR, NS>(c, La, lm, a, fg, a == 0);
-            else dispatch_pass<1, G, RR, NS>(c, La, lm, a, fg, a == 0);
+            if (F == 3) dispatch_pass<3, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
+            else if (F == 2) dispatch_pass<2, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
+            else dispatch_pass<1, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
             a += F;
             T -= F;
             fg = false;
@@ -627,12 +651,12 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         c.ystart = (k >> (D - a)) << (nv - a);
         if (Ffin == 2) {
             c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
-            dispatch_final<S, 2, G, RR, NS, LDS>(c, &lastlv, v, fg, a == 0);
+            dispatch_final<S, 2, G, RR, NS, LDS, YL>(c, &lastlv, v, fg, a == 0);
         } else if (a > 0) {
             c.src = lastlv;
-            dispatch_final<S, 1, G, RR, NS, LDS>(c, &lastlv, v, fg, false);
+            dispatch_final<S, 1, G, RR, NS, LDS, YL>(c, &lastlv, v, fg, false);
         } else {
-            dispatch_final<S, 1, G, RR, NS, LDS>(c, &lastlv, v, fg, true);
+            dispatch_final<S, 1, G, RR, NS, LDS, YL>(c, &lastlv, v, fg, true);
         }
         if (e0 == D) {  // the register subtree itself is rate-0 (its level-D values go unused)
             y = W::frozen(ub, fv, j) & SMASK;
@@ -642,9 +666,9 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         }
         // local encoding bits of virtual subtree k
         const int lstart = k * S;
-        uint32_t* yw = Y + (long long)(lstart >> 5) * ns;
-        if (S == 32) stu(yw, y);
-        else stu(yw, ((lstart & 31) == 0 ? 0u : (ldu(yw) & ((1u << (lstart & 31)) - 1u))) | (y << (lstart & 31)));
+        uint32_t* yw = Y + (long long)(lstart >> 5) * ys;
+        if (S == 32) sty<YL>(yw, y);
+        else sty<YL>(yw, ((lstart & 31) == 0 ? 0u : (ldy<YL>(yw) & ((1u << (lstart & 31)) - 1u))) | (y << (lstart & 31)));
         if (A.uout && store && j == 0) {
 #pragma unroll
             for (int w = 0; w < NW; ++w) {
@@ -680,17 +704,17 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
             const int Lc = Nv >> d;
             if (Lc < 32) {  // parent fits in one word (S < 32, deepest levels)
                 const int pstart = (k >> (D - d + 1)) * 2 * Lc;
-                uint32_t* pw = Y + (long long)(pstart >> 5) * ns;
-                const uint32_t w0 = ldu(pw);
+                uint32_t* pw = Y + (long long)(pstart >> 5) * ys;
+                const uint32_t w0 = ldy<YL>(pw);
                 const uint32_t w = w0 >> (pstart & 31);
                 const uint32_t lm = (1u << Lc) - 1u;
-                stu(pw, w0 ^ (((w >> Lc) & lm) << (pstart & 31)));
+                sty<YL>(pw, w0 ^ (((w >> Lc) & lm) << (pstart & 31)));
                 continue;
             }
             const int Wc = Lc >> 5;
-            uint32_t* base = Y + (long long)((k >> (D - d + 1)) * (2 * Wc)) * ns;
+            uint32_t* base = Y + (long long)((k >> (D - d + 1)) * (2 * Wc)) * ys;
             for (int w = 0; w < Wc; ++w)
-                stu(base + (long long)w * ns, ldu(base + (long long)w * ns) ^ ldu(base + (long long)(w + Wc) * ns));
+                sty<YL>(base + (long long)w * ys, ldy<YL>(base + (long long)w * ys) ^ ldy<YL>(base + (long long)(w + Wc) * ys));
         }
     }
     if (nacc && store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
@@ -702,7 +726,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
             uint32_t o = 0;
             for (int t = 0; t < 32; ++t) {
                 const uint32_t p = bitrev((uint32_t)(32 * w + t), nv);
-                o |= ((ldu(Y + (long long)(p >> 5) * ns) >> (p & 31u)) & 1u) << t;
+                o |= ((ldy<YL>(Y + (long long)(p >> 5) * ys) >> (p & 31u)) & 1u) << t;
             }
             A.xhat[(long long)(seg * W + w) * B + cw] = o;
         }

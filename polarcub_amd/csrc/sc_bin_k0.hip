@@ -11,6 +11,7 @@ BinKernFn bin_kernel_part0(int v) {
         case 12: return k_sc_bin<16, 2, 4, false, 1>;
         case 16: return k_sc_bin<32, 2, 2, false, 1>;
         case 20: return k_sc_bin<32, 8, 3, false, 1>;
+        case 24: return k_sc_bin<32, 4, 3, false, 1, true>;
         default: return nullptr;
     }
 }

@@ -11,6 +11,7 @@ BinKernFn bin_kernel_part1(int v) {
         case 13: return k_sc_bin<16, 4, 4, false, 1>;
         case 17: return k_sc_bin<32, 4, 3, false, 1>;
         case 21: return k_sc_bin<32, 16, 2, false, 1>;
+        case 25: return k_sc_bin<32, 8, 3, false, 1, true>;
         default: return nullptr;
     }
 }

@@ -15,24 +15,32 @@ constexpr int kBinBlock = 256;
 // per codeword G, and the minimum waves/SIMD the register allocation must allow.
 // Variant fields: S = register subtree values per lane, G = lanes per codeword,
 // W = minimum waves/SIMD for register allocation, L = deepest stage level in
-// LDS, T = non-temporal loads for the (once-streamed) input rows.
+// LDS, T = non-temporal loads for the (once-streamed) input rows, Y = the re-encoded bits
+// in LDS (Nv/32 words per thread; only where W workgroups still fit a CU's LDS).
 struct Variant {
-    int S, G, W, L, T;
+    int S, G, W, L, T, Y;
 };
-constexpr int kNumVariants = 24;
+constexpr int kNumVariants = 26;
 constexpr Variant kVar[kNumVariants] = {
     {16, 1, 2, 0, 0}, {8, 1, 4, 0, 0}, {32, 1, 1, 0, 0}, {16, 4, 2, 0, 0}, {8, 4, 4, 0, 0}, {16, 2, 2, 0, 0},
     {32, 2, 1, 0, 0}, {8, 8, 4, 0, 0}, {16, 2, 2, 0, 1}, {8, 8, 4, 0, 1}, {16, 4, 2, 0, 1}, {8, 4, 4, 1, 0},
     {16, 2, 4, 0, 1}, {16, 4, 4, 0, 1}, {8, 4, 4, 0, 1}, {32, 4, 2, 0, 1}, {32, 2, 2, 0, 1},
     {32, 4, 3, 0, 1}, {32, 2, 3, 0, 1}, {32, 8, 2, 0, 1}, {32, 8, 3, 0, 1},
     {32, 16, 2, 0, 1}, {32, 16, 3, 0, 1}, {16, 16, 3, 0, 1},
+    {32, 4, 3, 0, 1, 1}, {32, 8, 3, 0, 1, 1},
 };
 
 inline size_t bin_lds_bytes(int v) { return kVar[v].L ? (size_t)kVar[v].S * kBinBlock * sizeof(double2) : 0; }
 
-template <int S, int G, int W, bool LDS, int NT>
+// LDS bytes of the re-encoded bits of variant v at code length 2^n (0 unless Y)
+inline size_t bin_ylds_bytes(int v, int n) {
+    return kVar[v].Y ? (size_t)kBinBlock * (((size_t)1 << n) / kVar[v].G / 32) * sizeof(uint32_t) : 0;
+}
+
+template <int S, int G, int W, bool LDS, int NT, bool YL = false>
 __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
-    extern __shared__ double2 lds_last[];  // [S pairs][kBinBlock] when LDS (plus occupancy padding)
+    // [S pairs][kBinBlock] when LDS, then [Nv/32 words][kBinBlock] when YL (plus occupancy padding)
+    extern __shared__ double2 lds_last[];
     constexpr int CWB = kBinBlock / G;  // codewords per workgroup tile
     const long long slot = (long long)blockIdx.x * kBinBlock + threadIdx.x;
     const int j = threadIdx.x & (G - 1);
@@ -42,7 +50,9 @@ __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_codeword<S, G, LDS, NT>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last);
+        decode_codeword<S, G, LDS, NT, YL>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last,
+                                           YL ? (uint32_t*)(lds_last + (LDS ? S * kBinBlock : 0)) + threadIdx.x : nullptr,
+                                           kBinBlock);
     }
 }
 

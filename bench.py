@@ -322,6 +322,8 @@ class Qary:
             sc.set_qary_lanes(a.qlanes)
         if a.qregs:
             sc.set_qary_regs(a.qregs)
+        if a.qlds is not None:
+            sc.set_qary_lds(bool(a.qlds))
 
         self.dec = sc.QaryDecoder(self.code)
         gen = torch.Generator(device=device)
@@ -522,6 +524,7 @@ def build_parser():
     ap.add_argument("--qsc-p", type=float, default=0.11)
     ap.add_argument("--qlanes", type=int, default=0, help="q-ary: lanes per codeword (0 = the library's)")
     ap.add_argument("--qregs", type=int, default=0, help="q-ary: cap on register positions per lane (0 = the library's)")
+    ap.add_argument("--qlds", type=int, default=None, help="q-ary: re-encoded symbols in LDS (1) or in the workspace (0)")
     ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU")
     ap.add_argument("--variant", type=int, default=None, help="binary decode kernel variant (default: the library's)")
     ap.add_argument("--max-blocks", type=int, default=0, help="cap decode workgroups per CU (0 = occupancy)")

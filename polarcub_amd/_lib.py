@@ -44,6 +44,8 @@ def lib():
     L.pcub_sc_set_qary_lanes.argtypes = [ctypes.c_int]
     L.pcub_sc_set_qary_regs.restype = ctypes.c_int
     L.pcub_sc_set_qary_regs.argtypes = [ctypes.c_int]
+    L.pcub_sc_set_qary_lds.restype = ctypes.c_int
+    L.pcub_sc_set_qary_lds.argtypes = [ctypes.c_int]
     L.pcub_sc_num_variants.restype = ctypes.c_int
     L.pcub_sc_num_variants.argtypes = []
     L.pcub_sc_variant_info.restype = ctypes.c_int

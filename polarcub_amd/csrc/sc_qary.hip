@@ -69,15 +69,21 @@ __global__ __launch_bounds__(kQBlock) void k_encode_qary(const uint8_t* info, lo
 }
 
 int g_qlanes = 4;  // requested lanes per codeword (pcub_sc_set_qary_lanes)
+int g_qylds = 1;   // symbols in LDS where a twin kernel exists and fits (pcub_sc_set_qary_lds)
+constexpr size_t kQLdsPerCu = 160 * 1024;
 int g_qregs = 0;   // cap on register positions per lane (pcub_sc_set_qary_regs; 0 = the default)
 
 // register positions per lane S and lanes per codeword G for a code of 2^n:
 // S = 8 (q <= 4) or 4, G = the requested lanes, both reduced until N >= 2*S*G
 struct QGeom {
     int S, G;
+    bool yl;  // symbols in LDS
 };
+
+// LDS bytes of a workgroup's symbols: Nv/4 words per thread
+size_t qsym_lds_bytes(int n, int G) { return (size_t)kQBlock * ((((size_t)1 << n) / G + 3) / 4) * sizeof(uint32_t); }
 QGeom q_geom(int q, int n) {
-    QGeom c{4, g_qlanes};  // 8 register positions (q <= 4) via pcub_sc_set_qary_regs
+    QGeom c{4, g_qlanes, false};  // 8 register positions (q <= 4) via pcub_sc_set_qary_regs
     if (g_qregs > 0) c.S = (q <= 4 || g_qregs <= 4) ? g_qregs : 4;
     while (c.G > 1 && (1 << n) < 2 * c.S * c.G) c.G >>= 1;
     while (c.S > 1 && (1 << n) < 2 * c.S * c.G) c.S >>= 1;
@@ -86,13 +92,21 @@ QGeom q_geom(int q, int n) {
         c.G = 4;
         while (c.G > 1 && (1 << n) < 2 * c.S * c.G) c.G >>= 1;
     }
+    // symbols in LDS while the resident workgroups' columns fit the CU's LDS (N <= 512 at G = 4)
+    c.yl = g_qylds && qary_kernel_y(q, c.S, c.G) &&
+           (size_t)qary_waves(q, c.S, c.G) * qsym_lds_bytes(n, c.G) <= kQLdsPerCu;
     return c;
 }
 
 QKern qkernel(int q, int n, int* waves = nullptr) {
     const QGeom c = q_geom(q, n);
     if (waves) *waves = qary_waves(q, c.S, c.G);
-    return qary_kernel(q, c.S, c.G);
+    return c.yl ? qary_kernel_y(q, c.S, c.G) : qary_kernel(q, c.S, c.G);
+}
+
+size_t qlaunch_lds(int q, int n) {
+    const QGeom c = q_geom(q, n);
+    return c.yl ? qsym_lds_bytes(n, c.G) : 0;
 }
 
 long long qgrid(long long B, int q, int n) {
@@ -101,11 +115,13 @@ long long qgrid(long long B, int q, int n) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     int waves = 1;
     const QKern kern = qkernel(q, n, &waves);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kQBlock, 0) != hipSuccess || occ < 1) occ = 1;
+    const size_t lds = qlaunch_lds(q, n);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kQBlock, lds) != hipSuccess || occ < 1) occ = 1;
     // the launch bounds guarantee `waves` resident workgroups per CU (the occupancy
     // query under-reports these kernels on ROCm 7.2)
     const QGeom cg = q_geom(q, n);
     if (occ < waves) occ = waves;
+    if (lds > 0 && (size_t)occ * lds > kQLdsPerCu) occ = (int)(kQLdsPerCu / lds);
     const long long cwb = kQBlock / cg.G;
     const long long ntiles = (B + cwb - 1) / cwb;
     const long long g = (long long)cus * occ;
@@ -113,10 +129,11 @@ long long qgrid(long long B, int q, int n) {
 }
 
 // per lane: virtual stage levels 1..D-1 (Nv - 2S positions as pairs) + Nv symbol bytes in words
+// (unless the symbols are in LDS)
 size_t qslot_bytes(int n, int q) {
     const QGeom c = q_geom(q, n);
     const size_t Nv = ((size_t)1 << n) / c.G;
-    return (Nv - 2 * c.S) * (size_t)((q + 1) / 2) * sizeof(double2) + ((Nv + 3) & ~(size_t)3);
+    return (Nv - 2 * c.S) * (size_t)((q + 1) / 2) * sizeof(double2) + (c.yl ? 0 : ((Nv + 3) & ~(size_t)3));
 }
 
 int q_depth(int n, int q) {
@@ -170,8 +187,8 @@ extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, i
     A.nslots = g * kQBlock;
     char* slots = (char*)workspace + tb;
     A.scratch = (double2*)slots;
-    A.ysym = (uint32_t*)(slots + (size_t)A.nslots * (N / c.G - 2 * c.S) * ((q + 1) / 2) * sizeof(double2));
-    hipLaunchKernelGGL(qkernel(q, log2N), dim3((unsigned)g), dim3(kQBlock), 0, st, A);
+    A.ysym = c.yl ? nullptr : (uint32_t*)(slots + (size_t)A.nslots * (N / c.G - 2 * c.S) * ((q + 1) / 2) * sizeof(double2));
+    hipLaunchKernelGGL(qkernel(q, log2N), dim3((unsigned)g), dim3(kQBlock), qlaunch_lds(q, log2N), st, A);
     return (int)hipGetLastError();
 }
 
@@ -192,6 +209,15 @@ extern "C" int pcub_sc_set_qary_lanes(int G) {
     if (G != 1 && G != 2 && G != 4 && G != 8 && G != 16) return PCUB_EINVAL;
     const int old = g_qlanes;
     g_qlanes = G;
+    return old;
+}
+
+// Tuning hook (not part of the stable ABI): re-encoded symbols in LDS where a kernel for it
+// exists and fits (1, the default) or in the per-slot workspace (0).  Returns the previous value.
+extern "C" int pcub_sc_set_qary_lds(int on) {
+    if (on != 0 && on != 1) return PCUB_EINVAL;
+    const int old = g_qylds;
+    g_qylds = on;
     return old;
 }
 

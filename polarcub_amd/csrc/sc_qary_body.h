@@ -166,8 +166,10 @@ PCUB_HD void q_combine_words(uint32_t& m, uint32_t& p) {
     m = mm;
 }
 
+// YL: the symbols live in LDS (this thread's column, ldy/sty of sc_bin_body.h)
+template <bool YL = false>
 PCUB_HD int q_sym(const uint32_t* Y, long long ns, int pos) {
-    return (int)((ldu(Y + (long long)(pos >> 2) * ns) >> ((pos & 3) * 8)) & 0xffu);
+    return (int)((ldy<YL>(Y + (long long)(pos >> 2) * ns) >> ((pos & 3) * 8)) & 0xffu);
 }
 
 // Decisions of the register subtree: information symbols go out in u order
@@ -305,7 +307,8 @@ struct QPass {
     const double2* src;   // stored source level (a > 0)
     double2* lev[4];      // destinations: levels a+1 .. a+F (stored ones)
     long long ns;
-    const uint32_t* Y;    // re-encoded symbols (plus transform decisions)
+    const uint32_t* Y;    // re-encoded symbols (plus transform decisions), word w at Y[w * ys]
+    long long ys;
     int ystart;           // first Y position of the minus child at depth a+1
 };
 
@@ -317,18 +320,18 @@ PCUB_HD QV<Q> q_src(const QPass& P, int pos) {
 
 // Value of level a+E at index M of column c (position c + M*C), depth-first; every
 // level below a+F, and a+F itself unless FINAL, is stored on the way.
-template <int Q, int F, int E, int M, bool GOP, bool ROOT, bool FINAL>
+template <int Q, int F, int E, int M, bool GOP, bool ROOT, bool FINAL, bool YL>
 struct QCol {
     static PCUB_HD QV<Q> run(const QPass& P, int c, int C) {
         QV<Q> v;
         if constexpr (E == 1) {
             const QV<Q> x0 = q_src<Q, ROOT>(P, c + M * C);
             const QV<Q> x1 = q_src<Q, ROOT>(P, c + (M + (1 << (F - 1))) * C);
-            if constexpr (GOP) v = q_plus<Q>(x0, x1, q_sym(P.Y, P.ns, P.ystart + c + M * C));
+            if constexpr (GOP) v = q_plus<Q>(x0, x1, q_sym<YL>(P.Y, P.ys, P.ystart + c + M * C));
             else v = q_minus<Q>(x0, x1);
         } else {
-            const QV<Q> l = QCol<Q, F, E - 1, M, GOP, ROOT, FINAL>::run(P, c, C);
-            const QV<Q> r = QCol<Q, F, E - 1, M + (1 << (F - E)), GOP, ROOT, FINAL>::run(P, c, C);
+            const QV<Q> l = QCol<Q, F, E - 1, M, GOP, ROOT, FINAL, YL>::run(P, c, C);
+            const QV<Q> r = QCol<Q, F, E - 1, M + (1 << (F - E)), GOP, ROOT, FINAL, YL>::run(P, c, C);
             v = q_minus<Q>(l, r);
         }
         if constexpr (E < F || !FINAL) q_store2<Q>(P.lev[E - 1], c + M * C, P.ns, v);
@@ -338,50 +341,50 @@ struct QCol {
 
 // Non-final pass over all La >> F columns (U columns per iteration: loads of the
 // next column in flight while the current one computes).
-template <int Q, int F, bool GOP, bool ROOT, int U = 1>
+template <int Q, int F, bool GOP, bool ROOT, int U = 1, bool YL = false>
 PCUB_HD void q_pass(const QPass& P, int La) {
     const int C = La >> F;
     if constexpr (U == 1) {
 #pragma unroll 1
-        for (int c = 0; c < C; ++c) QCol<Q, F, F, 0, GOP, ROOT, false>::run(P, c, C);
+        for (int c = 0; c < C; ++c) QCol<Q, F, F, 0, GOP, ROOT, false, YL>::run(P, c, C);
     } else {
         int c = 0;
 #pragma unroll 1
         for (; c + U <= C; c += U) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) QCol<Q, F, F, 0, GOP, ROOT, false>::run(P, c + u, C);
+            for (int u = 0; u < U; ++u) QCol<Q, F, F, 0, GOP, ROOT, false, YL>::run(P, c + u, C);
         }
 #pragma unroll 1
-        for (; c < C; ++c) QCol<Q, F, F, 0, GOP, ROOT, false>::run(P, c, C);
+        for (; c < C; ++c) QCol<Q, F, F, 0, GOP, ROOT, false, YL>::run(P, c, C);
     }
 }
 
 // Final pass: level D (S values) into registers.
-template <int Q, int S, int F, bool GOP, bool ROOT>
+template <int Q, int S, int F, bool GOP, bool ROOT, bool YL>
 PCUB_HD void q_final(const QPass& P, QV<Q>* v) {
 #pragma unroll
-    for (int c = 0; c < S; ++c) v[c] = QCol<Q, F, F, 0, GOP, ROOT, true>::run(P, c, S);
+    for (int c = 0; c < S; ++c) v[c] = QCol<Q, F, F, 0, GOP, ROOT, true, YL>::run(P, c, S);
 }
 
-template <int Q, int F, int U>
+template <int Q, int F, int U, bool YL>
 PCUB_HD void q_pass_dispatch(const QPass& P, int La, bool gop, bool root) {
     if (root) {
-        if (gop) q_pass<Q, F, true, true, U>(P, La);
-        else q_pass<Q, F, false, true, U>(P, La);
+        if (gop) q_pass<Q, F, true, true, U, YL>(P, La);
+        else q_pass<Q, F, false, true, U, YL>(P, La);
     } else {
-        if (gop) q_pass<Q, F, true, false, U>(P, La);
-        else q_pass<Q, F, false, false, U>(P, La);
+        if (gop) q_pass<Q, F, true, false, U, YL>(P, La);
+        else q_pass<Q, F, false, false, U, YL>(P, La);
     }
 }
 
-template <int Q, int S, int F>
+template <int Q, int S, int F, bool YL>
 PCUB_HD void q_final_dispatch(const QPass& P, QV<Q>* v, bool gop, bool root) {
     if (root) {
-        if (gop) q_final<Q, S, F, true, true>(P, v);
-        else q_final<Q, S, F, false, true>(P, v);
+        if (gop) q_final<Q, S, F, true, true, YL>(P, v);
+        else q_final<Q, S, F, false, true, YL>(P, v);
     } else {
-        if (gop) q_final<Q, S, F, true, false>(P, v);
-        else q_final<Q, S, F, false, false>(P, v);
+        if (gop) q_final<Q, S, F, true, false, YL>(P, v);
+        else q_final<Q, S, F, false, false, YL>(P, v);
     }
 }
 
@@ -390,8 +393,10 @@ PCUB_HD void q_final_dispatch(const QPass& P, QV<Q>* v, bool gop, bool root) {
 // G = 8, 16 hold one or two more tree levels per codeword on chip than G = 4 (one
 // stored stage level fewer each) at the price of duplicated work in the cross-lane
 // leaf levels (both lanes of an exchanging pair evaluate the same transform).
-template <int Q, int S, int G = 1, int U = 1>
-PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store, int j = 0, int lane = 0) {
+// YL: the symbols in LDS (ylds = this thread's column, word w at ylds[w * ystride])
+template <int Q, int S, int G = 1, int U = 1, bool YL = false>
+PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store, int j = 0, int lane = 0,
+                            uint32_t* ylds = nullptr, long long ystride = 0) {
     constexpr int s = (S == 1) ? 0 : (S == 2) ? 1 : (S == 4) ? 2 : (S == 8) ? 3 : 4;
     constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : (G == 4) ? 2 : (G == 8) ? 3 : 4;
     constexpr int SU = S * G;  // real u positions per register subtree
@@ -403,14 +408,15 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
     const long long ns = A.nslots;
     const int D = nv - s;  // depth of the register nodes
     double2* scr = A.scratch + slot;
-    uint32_t* Y = A.ysym + slot;
+    uint32_t* Y = YL ? ylds : A.ysym + slot;
+    const long long ys = YL ? ystride : ns;  // symbol word stride
     // root rows of lane j: real position j + G*t is row bitrev_n(j) + bitrev_{nv}(t)
     const double* in = A.xy + (cw + (long long)bitrev((uint32_t)j, A.n) * A.B) * Q;
     QInfo qi{A.info, A.B, cw, store, 0, j, G - 1, 0u};
     for (int k = 0; k < (1 << D); ++k) {
         in = launder(in);
         scr = launder(scr);
-        Y = launder(Y);
+        if constexpr (!YL) Y = launder(Y);
         const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
         const int e0 = A.ef[k];  // first all-frozen depth on this chain (D + 1: none)
         const int stop = e0 <= D ? e0 - 1 : D;  // deepest level to evaluate
@@ -422,6 +428,7 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
         P.nv = nv;
         P.ns = ns;
         P.Y = Y;
+        P.ys = ys;
         // passes of up to three levels, greedily from the top; the last one (when the
         // chain reaches depth D) lands in registers
         while (true) {
@@ -437,9 +444,9 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
                 P.lev[e - 1] = (a + e < D) ? scr + (long long)(Nv - 2 * (Nv >> (a + e))) * QP * ns : nullptr;
             if (fin) break;
             const int La = Nv >> a;
-            if (F == 3) q_pass_dispatch<Q, 3, U>(P, La, gop, a == 0);
-            else if (F == 2) q_pass_dispatch<Q, 2, U>(P, La, gop, a == 0);
-            else q_pass_dispatch<Q, 1, U>(P, La, gop, a == 0);
+            if (F == 3) q_pass_dispatch<Q, 3, U, YL>(P, La, gop, a == 0);
+            else if (F == 2) q_pass_dispatch<Q, 2, U, YL>(P, La, gop, a == 0);
+            else q_pass_dispatch<Q, 1, U, YL>(P, La, gop, a == 0);
             a += F;
             gop = false;
         }
@@ -447,9 +454,9 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
         if (stop == D) {
             QV<Q> v[S];
             const int F = D - a;
-            if (F == 3) q_final_dispatch<Q, S, 3>(P, v, gop, a == 0);
-            else if (F == 2) q_final_dispatch<Q, S, 2>(P, v, gop, a == 0);
-            else q_final_dispatch<Q, S, 1>(P, v, gop, a == 0);
+            if (F == 3) q_final_dispatch<Q, S, 3, YL>(P, v, gop, a == 0);
+            else if (F == 2) q_final_dispatch<Q, S, 2, YL>(P, v, gop, a == 0);
+            else q_final_dispatch<Q, S, 1, YL>(P, v, gop, a == 0);
             const int us = k * SU;
             if constexpr (SU == 64) qi.fm = (uint64_t)A.fwords[us >> 5] | ((uint64_t)A.fwords[(us >> 5) + 1] << 32);
             else qi.fm = (uint64_t)(A.fwords[us >> 5] >> (us & 31));
@@ -462,15 +469,15 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
         if constexpr (S >= 4) {
 #pragma unroll
             for (int w = 0; w < S / 4; ++w)
-                stu(Y + (long long)(k * S / 4 + w) * ns, (uint32_t)y[4 * w] | ((uint32_t)y[4 * w + 1] << 8) |
+                sty<YL>(Y + (long long)(k * S / 4 + w) * ys, (uint32_t)y[4 * w] | ((uint32_t)y[4 * w + 1] << 8) |
                                                              ((uint32_t)y[4 * w + 2] << 16) | ((uint32_t)y[4 * w + 3] << 24));
         } else {
-            uint32_t* yw = Y + (long long)((k * S) >> 2) * ns;
+            uint32_t* yw = Y + (long long)((k * S) >> 2) * ys;
             const int sh = ((k * S) & 3) * 8;
             uint32_t ws = 0;
 #pragma unroll
             for (int t = 0; t < S; ++t) ws |= (uint32_t)y[t] << (8 * t);
-            stu(yw, (sh == 0 ? 0u : (ldu(yw) & ((1u << sh) - 1u))) | (ws << sh));
+            sty<YL>(yw, (sh == 0 ? 0u : (ldy<YL>(yw) & ((1u << sh) - 1u))) | (ws << sh));
         }
         // combine completed plus children: [(ym+yp)%q | (q-yp)%q]
         for (int d = D; d >= 1 && ((k >> (D - d)) & 1); --d) {
@@ -478,21 +485,21 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
             const long long st = (long long)(k >> (D - d + 1)) * 2 * Lc;
             if (Lc >= 4) {
                 for (int w = 0; w < Lc / 4; ++w) {
-                    uint32_t* pm = Y + (st / 4 + w) * ns;
-                    uint32_t* pp = Y + (st / 4 + Lc / 4 + w) * ns;
-                    uint32_t m = ldu(pm), p = ldu(pp);
+                    uint32_t* pm = Y + (st / 4 + w) * ys;
+                    uint32_t* pp = Y + (st / 4 + Lc / 4 + w) * ys;
+                    uint32_t m = ldy<YL>(pm), p = ldy<YL>(pp);
                     q_combine_words<Q>(m, p);
-                    stu(pm, m);
-                    stu(pp, p);
+                    sty<YL>(pm, m);
+                    sty<YL>(pp, p);
                 }
             } else {  // Lc = 1, 2: the parent is 2 or 4 bytes of one word
-                uint32_t* pw = Y + (st >> 2) * ns;
+                uint32_t* pw = Y + (st >> 2) * ys;
                 const int sh = (int)(st & 3) * 8;
                 const uint32_t lm = (Lc == 1) ? 0xffu : 0xffffu;
-                const uint32_t w0 = ldu(pw);
+                const uint32_t w0 = ldy<YL>(pw);
                 uint32_t m = (w0 >> sh) & lm, p = (w0 >> (sh + 8 * Lc)) & lm;
                 q_combine_words<Q>(m, p);
-                stu(pw, (w0 & ~(((lm << (8 * Lc)) | lm) << sh)) | (((p << (8 * Lc)) | m) << sh));
+                sty<YL>(pw, (w0 & ~(((lm << (8 * Lc)) | lm) << sh)) | (((p << (8 * Lc)) | m) << sh));
             }
         }
     }
@@ -500,7 +507,7 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
     // bitrev_n(j) + bitrev_{nv}(t), t = its local position
     if (A.xhat && store) {
         uint8_t* xo = A.xhat + cw + (long long)bitrev((uint32_t)j, A.n) * A.B;
-        for (int t = 0; t < Nv; ++t) xo[(long long)bitrev((uint32_t)t, nv) * A.B] = (uint8_t)q_sym(Y, ns, t);
+        for (int t = 0; t < Nv; ++t) xo[(long long)bitrev((uint32_t)t, nv) * A.B] = (uint8_t)q_sym<YL>(Y, ys, t);
     }
 }
 

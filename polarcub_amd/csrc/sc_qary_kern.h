@@ -23,8 +23,10 @@ constexpr int qary_waves(int q, int S, int G = 4) {
     return (G >= 8 && q * S == 32 && q < 6) ? 3 : (q * S >= 32 || q >= 6) ? 2 : (q * S <= 16 ? 4 : 3);
 }
 
-template <int Q, int S, int G, int W = qary_waves(Q, S, G), int U = 1>
+// YL: the re-encoded symbols in dynamic LDS ([Nv/4 words][kQaryBlock]) instead of the slot
+template <int Q, int S, int G, int W = qary_waves(Q, S, G), int U = 1, bool YL = false>
 __global__ __launch_bounds__(kQaryBlock, W) void k_sc_qary(QArgs A) {
+    extern __shared__ uint32_t qsym_lds[];
     constexpr int CWB = kQaryBlock / G;  // codewords per tile
     const long long slot = (long long)blockIdx.x * kQaryBlock + threadIdx.x;
     const int j = threadIdx.x & (G - 1);
@@ -33,7 +35,8 @@ __global__ __launch_bounds__(kQaryBlock, W) void k_sc_qary(QArgs A) {
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_qary_cw<Q, S, G, U>(A, valid ? cw : A.B - 1, slot, valid, j, lane);
+        decode_qary_cw<Q, S, G, U, YL>(A, valid ? cw : A.B - 1, slot, valid, j, lane,
+                                       YL ? qsym_lds + threadIdx.x : nullptr, kQaryBlock);
     }
 }
 
@@ -45,6 +48,10 @@ QKern qary_kernel_q3(int S, int G);
 QKern qary_kernel_q4(int S, int G);
 QKern qary_kernel_q56(int q, int S, int G);
 QKern qary_kernel_q78(int q, int S, int G);
+
+// the symbols-in-LDS twin of the kernel for (q, S, G), or nullptr (q = 4, S = 4, G = 4 only)
+QKern qary_kernel_q4_y(int S, int G);
+inline QKern qary_kernel_y(int q, int S, int G) { return q == 4 ? qary_kernel_q4_y(S, G) : nullptr; }
 
 inline QKern qary_kernel(int q, int S, int G) {
     switch (q) {

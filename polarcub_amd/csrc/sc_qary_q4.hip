@@ -19,4 +19,10 @@ QKern qary_kernel_q4(int S, int G) {
     return qary_kernel_geom<4, 8>(S, G);
 }
 
+// the C4 geometry with its symbols in LDS (16 words a thread at N = 256)
+QKern qary_kernel_q4_y(int S, int G) {
+    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, qary_waves(4, 4, 4), 1, true>;
+    return nullptr;
+}
+
 }  // namespace pcub

@@ -134,6 +134,15 @@ def set_qary_lanes(g):
     return old
 
 
+def set_qary_lds(on):
+    """Re-encoded symbols of the q-ary decode kernel in LDS where a kernel for it exists and
+    fits (True, the default) or in the per-slot workspace (False).  Returns the previous setting."""
+    old = int(_lib.lib().pcub_sc_set_qary_lds(1 if on else 0))
+    if old < 0:
+        raise ValueError("pcub_sc_set_qary_lds")
+    return bool(old)
+
+
 def set_qary_regs(s):
     """Cap on the q-ary decode kernel's register positions per lane (0 = default, 2, 4 or
     8).  Returns the previous setting."""

@@ -18,8 +18,11 @@ def lanes(request):
     sc.set_qary_lanes(old)
 
 
-def test_qsc_q4_n256_matches_reference(lanes):
+@pytest.mark.parametrize("lds", [True, False])
+def test_qsc_q4_n256_matches_reference(lanes, lds):
+    """lds: the re-encoded symbols in LDS (the C4 kernel's default) or in the workspace."""
     from polarcub_amd import sc
+    old_lds = sc.set_qary_lds(lds)
     g = load_golden("qsc_q4_n256")
     code = sc.QaryCode(4, 256, g["frozen"])
     dec = sc.QaryDecoder(code)
@@ -30,6 +33,7 @@ def test_qsc_q4_n256_matches_reference(lanes):
     # x_hat re-encodes the decoded symbols
     enc = sc.encode_qary(code, info)
     assert torch.equal(enc, xhat)
+    sc.set_qary_lds(old_lds)
 
 
 def test_qary_q3_matches_reference(lanes):

@@ -125,7 +125,9 @@ long long qgrid(long long B, int q, int n) {
     const long long cwb = kQBlock / cg.G;
     const long long ntiles = (B + cwb - 1) / cwb;
     const long long g = (long long)cus * occ;
-    return ntiles < g ? ntiles : g;
+    if (ntiles <= g) return ntiles;
+    const long long rounds = (ntiles + g - 1) / g;  // whole rounds (as the binary launcher)
+    return (ntiles + rounds - 1) / rounds;
 }
 
 // per lane: virtual stage levels 1..D-1 (Nv - 2S positions as pairs) + Nv symbol bytes in words

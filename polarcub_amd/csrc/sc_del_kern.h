@@ -357,10 +357,12 @@ __device__ __forceinline__ uint32_t del_n02_half(const Base02& b, const uint32_t
     Child02 c;
     n02_transform(b, dec, c);
     n02_normalize(c);
+    Paths02 q;
+    n02_paths(c, q);
     double m0, m1;
-    n02_collapse(c, nullptr, m0, m1);
+    n02_collapse_paths(q, nullptr, m0, m1);
     const uint32_t xm = cx.subtree(norm_pack(m0, m1));
-    n02_collapse(c, &xm, m0, m1);
+    n02_collapse_paths(q, &xm, m0, m1);
     const uint32_t xp = cx.subtree(norm_pack(m0, m1));
     return (xm ^ xp) | (xp << 1);
 }

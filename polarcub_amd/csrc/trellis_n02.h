@@ -241,4 +241,76 @@ PCUB_HD void n02_collapse(const Child02& c, const uint32_t* dec, double& m0, dou
     }
 }
 
+// The collapse's paths through each middle vertex, gathered once per (normalised) child: a
+// layer-1 vertex w has at most two edges start -> w (labels 0, 1; the start is the only
+// from-vertex) and two edges w -> end, so n02_collapse's 3 x 6 x 6 predicated scan becomes
+// 3 x 2 x 2.  Lists keep creation order, so the sums run in the same order.
+struct Paths02 {
+    int nin[kN02V], nout[kN02V];
+    double ip[kN02V][2], op[kN02V][2];
+    int il[kN02V][2], ol[kN02V][2];
+};
+
+PCUB_HD void n02_paths(const Child02& c, Paths02& q) {
+#pragma unroll
+    for (int wi = 0; wi < kN02V; ++wi) {
+        q.nin[wi] = 0;
+        q.nout[wi] = 0;
+        q.ip[wi][0] = q.ip[wi][1] = q.op[wi][0] = q.op[wi][1] = 0.0;
+        q.il[wi][0] = q.il[wi][1] = q.ol[wi][0] = q.ol[wi][1] = 0;
+        if (wi >= c.nw) continue;
+        const int w = c.w[wi];
+#pragma unroll
+        for (int a = 0; a < kN02E; ++a) {
+            if (a < c.n0 && (c.k0[a] >> 1) == w) {
+                if (q.nin[wi] == 0) {
+                    q.ip[wi][0] = c.p0[a];
+                    q.il[wi][0] = c.k0[a] & 1;
+                } else {
+                    q.ip[wi][1] = c.p0[a];
+                    q.il[wi][1] = c.k0[a] & 1;
+                }
+                ++q.nin[wi];
+            }
+            if (a < c.n1 && (c.k1[a] >> 1) == w) {
+                if (q.nout[wi] == 0) {
+                    q.op[wi][0] = c.p1[a];
+                    q.ol[wi][0] = c.k1[a] & 1;
+                } else {
+                    q.op[wi][1] = c.p1[a];
+                    q.ol[wi][1] = c.k1[a] & 1;
+                }
+                ++q.nout[wi];
+            }
+        }
+    }
+}
+
+// n02_collapse over the gathered paths (same terms, same order)
+PCUB_HD void n02_collapse_paths(const Paths02& q, const uint32_t* dec, double& m0, double& m1) {
+    m0 = 0.0;
+    m1 = 0.0;
+    const int dj = dec ? (int)(*dec & 1u) : 0;
+#pragma unroll
+    for (int wi = 0; wi < kN02V; ++wi) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            if (a >= q.nin[wi]) continue;
+#pragma unroll
+            for (int o = 0; o < 2; ++o) {
+                if (o >= q.nout[wi]) continue;
+                const double prob = q.ip[wi][a] * q.op[wi][o];
+                const int ml = q.il[wi][a] ^ q.ol[wi][o];
+                int x = ml;
+                if (dec) {
+                    if (ml != dj) continue;
+                    x = q.ol[wi][o];
+                }
+                if (x) m1 += prob;
+                else m0 += prob;
+            }
+        }
+    }
+}
+
 }  // namespace pcub

@@ -184,18 +184,27 @@ std::vector<uint32_t> decode_n02(const BitF& bit, int len, int tb, double pd, Ct
     std::vector<uint32_t> y[2];
     std::vector<double> vals(T);
     for (int half = 0; half < 2; ++half) {
+        // the kernel's collapse (gathered paths), checked against the full scan bit for bit
+        auto collapse = [](const Child02& ch, const uint32_t* dec, double& m0, double& m1) {
+            Paths02 q;
+            n02_paths(ch, q);
+            n02_collapse_paths(q, dec, m0, m1);
+            double r0, r1;
+            n02_collapse(ch, dec, r0, r1);
+            if (as_bits(r0) != as_bits(m0) || as_bits(r1) != as_bits(m1)) throw 5;
+        };
         for (int t = 0; t < T; ++t) {
             n02_transform(b[t], half ? &y[0][t] : nullptr, c[t]);
             n02_normalize(c[t]);
             double m0, m1;
-            n02_collapse(c[t], nullptr, m0, m1);
+            collapse(c[t], nullptr, m0, m1);
             vals[t] = norm_pack(m0, m1);
         }
         const std::vector<int> xm = mem_sc(vals, cx);
         for (int t = 0; t < T; ++t) {
             double m0, m1;
             const uint32_t d = (uint32_t)xm[t];
-            n02_collapse(c[t], &d, m0, m1);
+            collapse(c[t], &d, m0, m1);
             vals[t] = norm_pack(m0, m1);
         }
         const std::vector<int> xp = mem_sc(vals, cx);
@@ -288,6 +297,7 @@ extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, lon
             }
         } catch (int e) {
             return e == 4 ? -4    // the implicit base's child differs from the stored base's
+                 : e == 5 ? -5    // the n0 = 2 path-list collapse differs from the full scan
                           : -3;   // trellis_collapse disagrees with the materialised child's marginal
         }
         if ((int)cx.info.size() != K) return -2;

@@ -97,38 +97,39 @@ struct Child02 {
     int k1[kN02E];
     double p1[kN02E];
 
-    // Both are predicated (ok = this lane has the contribution): the lanes of a wave hold
-    // different segments, so a branch per contribution would diverge; selects do not.
-    PCUB_HD void vertex(bool ok, int v) {
+    PCUB_HD void vertex(int v) {
         bool have = false;
 #pragma unroll
-        for (int i = 0; i < kN02V; ++i) have = have | ((i < nw) & (w[i] == v));
-        const bool ins = ok & !have;
+        for (int i = 0; i < kN02V; ++i) have = have || (i < nw && w[i] == v);
+        if (!have) {
 #pragma unroll
-        for (int i = 0; i < kN02V; ++i) w[i] = (ins & (i == nw)) ? v : w[i];
-        nw += ins ? 1 : 0;
+            for (int i = 0; i < kN02V; ++i)
+                if (i == nw) w[i] = v;
+            ++nw;
+        }
     }
     // addToEdgeProb on edge layer J (BinaryTrellis.py:128-136): from-vertex, to-vertex, edge
     template <int J>
-    PCUB_HD void add(bool ok, int key, double p) {
+    PCUB_HD void add(int key, double p) {
         int(&k)[kN02E] = J ? k1 : k0;
         double(&pp)[kN02E] = J ? p1 : p0;
         int& n = J ? n1 : n0;
         bool found = false;
 #pragma unroll
-        for (int i = 0; i < kN02E; ++i) {
-            const bool hit = ok & (i < n) & (k[i] == key);
-            pp[i] = hit ? pp[i] + p : pp[i];
-            found = found | hit;
-        }
-        const bool ins = ok & !found;
+        for (int i = 0; i < kN02E; ++i)
+            if (i < n && k[i] == key) {
+                pp[i] += p;
+                found = true;
+            }
+        if (!found) {
 #pragma unroll
-        for (int i = 0; i < kN02E; ++i) {
-            const bool at = ins & (i == n);
-            k[i] = at ? key : k[i];
-            pp[i] = at ? 0.0 + p : pp[i];
+            for (int i = 0; i < kN02E; ++i)
+                if (i == n) {
+                    k[i] = key;
+                    pp[i] = 0.0 + p;
+                }
+            ++n;
         }
-        n += ins ? 1 : 0;
     }
 };
 
@@ -137,45 +138,41 @@ struct Child02 {
 PCUB_HD void n02_transform(const Base02& b, const uint32_t* dec, Child02& c) {
     c.nw = c.n0 = c.n1 = 0;
 #pragma unroll
-    for (int i = 0; i < kN02V; ++i) c.w[i] = -1;
-#pragma unroll
-    for (int i = 0; i < kN02E; ++i) {
-        c.k0[i] = c.k1[i] = -1;
-        c.p0[i] = c.p1[i] = 0.0;
-    }
-#pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int mid = 2 * j + 1;
         const int dj = dec ? (int)((*dec >> j) & 1u) : 0;
-        int ws[kN02V] = {-1, -1, -1};
+        int ws[kN02V];
         const int nws = b.layer(mid, ws);
 #pragma unroll
         for (int wi = 0; wi < kN02V; ++wi) {
-            const bool wok = wi < nws;
+            if (wi >= nws) continue;
             const int w = ws[wi];
             // in-edges of w: insertion from w-1, then deletions 0, 1 from w (creation order)
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 const int u = a == 0 ? w - 1 : w;
-                int tu = -1, lu = 0;
-                double pu = 0.0;
-                const bool ain = wok & b.out_edge(mid - 1, u, a, tu, lu, pu) & (tu == w);
+                int tu, lu;
+                double pu;
+                if (!b.out_edge(mid - 1, u, a, tu, lu, pu) || tu != w) continue;
 #pragma unroll
                 for (int o = 0; o < 3; ++o) {
-                    int tv = 0, lv = 0;
-                    double pv = 0.0;
-                    const bool oin = ain & b.out_edge(mid, w, o, tv, lv, pv);
+                    int tv, lv;
+                    double pv;
+                    if (!b.out_edge(mid, w, o, tv, lv, pv)) continue;
                     const double prob = pu * pv;
                     const int ml = lu ^ lv;
-                    const int x = dec ? lv : ml;
-                    const bool ok = oin & (!dec | (ml == dj));
+                    int x = ml;
+                    if (dec) {
+                        if (ml != dj) continue;
+                        x = lv;
+                    }
                     // new edge (u_layer_j, v_layer_j+1): j = 0 -> 0 -> tv; j = 1 -> u -> m
                     if (j == 0) {
-                        c.vertex(ok, tv);  // the from-vertex is the start (always present)
-                        c.template add<0>(ok, tv * 2 + x, prob);
+                        c.vertex(tv);  // the from-vertex is the start (always present)
+                        c.template add<0>(tv * 2 + x, prob);
                     } else {
-                        c.vertex(ok, u);   // the to-vertex is the end (always present)
-                        c.template add<1>(ok, u * 2 + x, prob);
+                        c.vertex(u);   // the to-vertex is the end (always present)
+                        c.template add<1>(u * 2 + x, prob);
                     }
                 }
             }

@@ -84,3 +84,24 @@ def test_list_decode_facade_single_word(sc):
         assert pr.name == c["prob_result"][t]
         if pr.name.startswith("Success"):
             assert np.array_equal(info, g[t_ + "_actual"][t])
+
+
+def test_gpu_list_decoder_full_occupancy(sc):
+    """A batch that fills every resident workgroup (2^17 codewords, q=4, N=256, L=8): the
+    recursion's dynamic stack must fit each wave's scratch at full occupancy (the runtime's
+    1 KiB default does not; the launcher raises it), and the first codewords decode as they
+    do alone."""
+    import torch
+    rng = np.random.default_rng(5)
+    q, n, L, B = 4, 8, 8, 1 << 17
+    N = 1 << n
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    dec = sc.QaryListDecoder(q, N, frozen, L)
+    xy = torch.rand((N, B, q), dtype=torch.float64, device="cuda")
+    fv = torch.zeros((int(frozen.sum()), B), dtype=torch.uint8, device="cuda")
+    info, prob, size, _ = dec.decode_native(xy, fv)
+    torch.cuda.synchronize()
+    assert int(size.min()) >= 1
+    info1, prob1, size1, _ = dec.decode_native(xy[:, :6].contiguous(), fv[:, :6].contiguous())
+    assert torch.equal(size[:6], size1)
+    assert torch.equal(info[:, :, :6], info1) and torch.equal(prob[:, :6], prob1)

@@ -99,7 +99,7 @@ class Awgn:
         frozen = construction.bhattacharyya_frozen(n, K, self.sigma2)
         self.code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(frozen)[0].tolist()), 1, device=device)
         sc.set_variant(a.variant)
-        self.variant = sc.default_variant() if a.variant is None else a.variant
+        self.variant = sc.variant_for(self.n)  # the kernel that runs (fallback included)
         sc.set_max_blocks_per_cu(a.max_blocks)
         self.dec = sc.BinaryDecoder(self.code)
         # global codewords [rank*B, (rank+1)*B), Philox keyed by (seed, codeword index)

@@ -37,6 +37,8 @@ def lib():
     L.pcub_sc_set_variant.restype = ctypes.c_int
     L.pcub_sc_default_variant.restype = ctypes.c_int
     L.pcub_sc_default_variant.argtypes = []
+    L.pcub_sc_variant_for.restype = ctypes.c_int
+    L.pcub_sc_variant_for.argtypes = [ctypes.c_int32]
     L.pcub_sc_set_variant.argtypes = [ctypes.c_int]
     L.pcub_sc_set_max_blocks_per_cu.restype = ctypes.c_int
     L.pcub_sc_set_max_blocks_per_cu.argtypes = [ctypes.c_int]

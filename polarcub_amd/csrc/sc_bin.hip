@@ -39,13 +39,15 @@ KernFn variant_kernel(int v) {
     if (KernFn k = bin_kernel_part0(v)) return k;
     if (KernFn k = bin_kernel_part1(v)) return k;
     if (KernFn k = bin_kernel_part2(v)) return k;
-    return bin_kernel_part3(v);
+    if (KernFn k = bin_kernel_part3(v)) return k;
+    return bin_kernel_part4(v);
 }
 
-// {32, 4, 3, NT, re-encoded bits in LDS}: fastest at N=1024 and N=4096 on MI355X
-// (73.9 / 13.3 M cw/s vs 72.0 / 12.5 M for its global-bits twin 17, profiles/r2/ylds/);
-// past the LDS budget (N > 4096) pick_variant falls back to 17
-constexpr int kDefaultVariant = 24;
+// {32, 4, 2, NT, re-encoded bits in LDS, split last level, prefetch 2}: at N=1024 one stored
+// stage depth fewer than variant 24 (48.7 vs 68.6 KB/cw of HBM traffic) at 2 waves/SIMD,
+// 76.3 vs 73.7 M cw/s (profiles/r3/); past its LDS budget (N > 1024 at G = 4) pick_variant
+// falls back to 24 {32, 4, 3, NT, bits in LDS} (N = 4096: 13.3 M cw/s), then to 17
+constexpr int kDefaultVariant = 26;
 int g_variant = kDefaultVariant;
 int g_max_blocks = 0;  // workgroups per CU cap (0 = as many as fit)
 constexpr size_t kLdsPerCu = 160 * 1024;
@@ -91,7 +93,7 @@ int tree_depth(int n, int v) {
     int g = 0;
     while ((1 << g) < kVar[v].G) ++g;
     int s = 0;
-    while ((1 << s) < kVar[v].S) ++s;
+    while ((1 << s) < bin_sr(v)) ++s;
     return n - g - s;
 }
 size_t ef_bytes(int n, int v) { return (((size_t)1 << tree_depth(n, v)) + 255) & ~(size_t)255; }
@@ -99,7 +101,7 @@ size_t ef_bytes(int n, int v) { return (((size_t)1 << tree_depth(n, v)) + 255) &
 // per-slot bytes: virtual levels 1..D-1 (Nv/2 - S pairs) + Nv local encoding bits (unless in LDS)
 size_t slot_bytes(int n, int v) {
     const size_t Nv = ((size_t)1 << n) / kVar[v].G;
-    return (Nv / 2 - kVar[v].S) * sizeof(double2) + (kVar[v].Y ? 0 : (Nv / 32) * sizeof(uint32_t));
+    return (Nv / 2 - bin_sr(v)) * sizeof(double2) + (kVar[v].Y ? 0 : (Nv / 32) * sizeof(uint32_t));
 }
 
 long long grid_for(long long B, int v, int n) {
@@ -124,11 +126,11 @@ long long grid_for(long long B, int v, int n) {
 bool fits(int v, int n) {
     const long long N = 1LL << n;
     if (kVar[v].Y && (size_t)kVar[v].W * launch_lds(v, n) > kLdsPerCu) return false;
-    return N >= 2LL * kVar[v].S * kVar[v].G && N >= 32LL * kVar[v].G;
+    return N >= 2LL * bin_sr(v) * kVar[v].G && N >= 32LL * kVar[v].G;
 }
 int pick_variant(int n) {
     if (fits(g_variant, n)) return g_variant;
-    constexpr int kFallback[] = {17, 13, 14, 10, 0, 1};
+    constexpr int kFallback[] = {24, 17, 13, 14, 10, 0, 1};
     for (int v : kFallback)
         if (fits(v, n)) return v;
     return 1;
@@ -154,6 +156,11 @@ extern "C" int pcub_sc_set_max_blocks_per_cu(int b) {
 }
 
 extern "C" int pcub_sc_default_variant(void) { return kDefaultVariant; }
+// the variant a decode of code length 2^log2N launches (the selected one, or its fallback)
+extern "C" int pcub_sc_variant_for(int32_t log2N) {
+    if (log2N < 6 || log2N > 24) return PCUB_EINVAL;
+    return pick_variant(log2N);
+}
 extern "C" int pcub_sc_set_variant(int v) {
     if (v < 0 || v >= kNumVariants) return PCUB_EINVAL;
     g_variant = v;
@@ -214,11 +221,11 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
     uint8_t* ef = (uint8_t*)workspace;
     char* slots = (char*)workspace + efb;
     hipLaunchKernelGGL(k_ef_table, dim3((unsigned)(((1 << D) + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, frozen_mask,
-                       D, kVar[v].S * kVar[v].G, ef);
+                       D, bin_sr(v) * kVar[v].G, ef);
     A.ef = ef;
     A.nslots = nslots;
     A.scratch = (double2*)slots;
-    A.ybits = kVar[v].Y ? nullptr : (uint32_t*)(slots + (size_t)nslots * (Nv / 2 - kVar[v].S) * sizeof(double2));
+    A.ybits = kVar[v].Y ? nullptr : (uint32_t*)(slots + (size_t)nslots * (Nv / 2 - bin_sr(v)) * sizeof(double2));
     hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), launch_lds(v, log2N), st, A);
     return (int)hipGetLastError();
 }

@@ -289,6 +289,26 @@ PCUB_HD void sty(uint32_t* p, uint32_t v) {
     stu(p, v);
 }
 
+// Split register level (HL variants): the first half of the chain's last level lives in
+// this thread's LDS column (value t at hl[t * kHlStride]), the second half in registers.
+constexpr int kHlStride = 256;  // = kBinBlock: one column per thread of the workgroup
+
+PCUB_HD void stl(double* p, double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *(__attribute__((address_space(3))) double*)p = v;
+#else
+    *p = v;
+#endif
+}
+
+PCUB_HD double ldl(const double* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(3))) double*)p;
+#else
+    return *p;
+#endif
+}
+
 // Root rows.  Local position t of lane j is real position p = j + G*t < N/2,
 // which pairs natural rows (2q, 2q+1) with q = bitrev_{n-1}(p).  The bits of j
 // and of G*t are disjoint, so q = bitrev_{n-1}(j) + bitrev_{nv-1}(t): the lane
@@ -315,158 +335,6 @@ PCUB_HD void sched_fence() {
 #endif
 }
 
-// Fused column pair.  From the depth-a node (La local values) evaluate F levels
-// for the two columns p, p+1 (p even) of stride C = La >> F: level a+e holds
-// positions p + m*C, m < 2^(F-e), and needs level a+e-1 at m and m + 2^(F-e).
-// The first op is a plus transform when FG (bits of the minus child), else a
-// minus transform; every later op is a minus transform (an SC chain descends
-// through minus children).  y receives levels a+1 .. a+F back to back
-// (2^(F-1), 2^(F-2), .., 1 entries; .x = column p, .y = column p+1).
-template <int F, bool FG, int R, int G, bool NS = false, bool GL = true, bool YL = false>
-PCUB_HD void colpair(const Chain& c, int p, int C, double2* y) {
-    constexpr bool ROOT = R != 0;
-    constexpr int H = 1 << (F - 1);
-#pragma unroll
-    for (int m = 0; m < H; ++m) {
-        const int P = p + m * C;
-        uint32_t u0 = 0, u1 = 0;
-        if (FG) {
-            const int bp = c.ystart + P;  // even: bits bp, bp+1 share a word
-            const uint32_t w = ldy<YL>(c.Y + (long long)(bp >> 5) * c.ns) >> (bp & 31);
-            u0 = w & 1u;
-            u1 = (w >> 1) & 1u;
-        }
-        double2 o;
-        if (ROOT) {
-            // positions P, P + Nv/2 are rows (2q, 2q+1); P+1 adds Nv/4 to q
-            const long long q0 = root_row(P, c.nv);
-            const long long q1 = q0 + (1LL << (c.nv - 2));
-            const double2 a0 = ld2<R == 2>(c.in + (2 * q0) * c.B);
-            const double2 b0 = ld2<R == 2>(c.in + (2 * q0 + 1) * c.B);
-            const double2 a1 = ld2<R == 2>(c.in + (2 * q1) * c.B);
-            const double2 b1 = ld2<R == 2>(c.in + (2 * q1 + 1) * c.B);
-            o.x = FG ? op_g_raw(a0, b0, u0) : op_f_raw(a0, b0);
-            o.y = FG ? op_g_raw(a1, b1, u1) : op_f_raw(a1, b1);
-        } else {
-            const double2 a = ld2<NS, GL>(c.src.p + (long long)(P >> 1) * c.src.s);
-            const double2 b = ld2<NS, GL>(c.src.p + (long long)((P + H * C) >> 1) * c.src.s);
-            o.x = FG ? op_g(a.x, b.x, u0) : op_f(a.x, b.x);
-            o.y = FG ? op_g(a.y, b.y, u1) : op_f(a.y, b.y);
-        }
-        y[m] = o;
-    }
-    int in_off = 0, out_off = H;
-#pragma unroll
-    for (int e = 2; e <= F; ++e) {
-        const int He = 1 << (F - e);
-#pragma unroll
-        for (int m = 0; m < He; ++m) {
-            y[out_off + m].x = op_f(y[in_off + m].x, y[in_off + m + He].x);
-            y[out_off + m].y = op_f(y[in_off + m].y, y[in_off + m + He].y);
-        }
-        in_off = out_off;
-        out_off += He;
-    }
-}
-
-// Where stored level d (1 <= d <= D-1) lives: the per-slot scratch, or `last` for d == D-1.
-struct LevelMap {
-    double2* scr;
-    long long ns;
-    int Nv;
-    int D;
-    Lvl last;
-    PCUB_HD Lvl get(int d) const {
-        if (last.p && d == D - 1) return last;
-        return Lvl{scr + (long long)(Nv / 2 - (Nv >> d)) * ns, ns};
-    }
-};
-
-// Non-final pass: levels a+1 .. a+F are all stored.
-template <int F, bool FG, int R, int G, bool NS, bool YL>
-PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
-    Lvl lv[F];
-#pragma unroll
-    for (int e = 1; e <= F; ++e) lv[e - 1] = lm.get(a + e);
-    const int C = La >> F;
-#pragma unroll 1
-    for (int p = 0; p < C; p += 2) {
-        double2 y[(1 << F) - 1];
-        colpair<F, FG, R, G, NS, true, YL>(c, p, C, y);
-        int off = 0;
-#pragma unroll
-        for (int e = 1; e <= F; ++e) {
-            const int He = 1 << (F - e);
-#pragma unroll
-            for (int m = 0; m < He; ++m) st2<NS>(lv[e - 1].p + (long long)((p + m * C) >> 1) * lv[e - 1].s, y[off + m]);
-            off += He;
-        }
-    }
-}
-
-// Final pass into registers (F = 1 or 2): with F = 2, level D-1 is stored to
-// lv[0]; level D (S values) goes into v.  Level D-1 is touched only by final
-// passes (stored here, or read as c.src when F = 1), which lets it live in LDS
-// with static addressing.  (A three-level final pass from the root needs more
-// than the 168 VGPRs of three waves/SIMD with S = 32 and spills.)
-template <int S, int F, bool FG, int R, int G, bool NS, bool LL, bool YL>
-PCUB_HD void chain_final(const Chain& c, const Lvl* lv, double* v) {
-    static_assert(F == 1 || F == 2, "final pass fuses at most two levels");
-#pragma unroll
-    for (int p = 0; p < S; p += 2) {
-        double2 y[(1 << F) - 1];
-        colpair<F, FG, R, G, NS && F == 2, F == 2 || !LL, YL>(c, p, S, y);
-        if constexpr (F == 2) {
-#pragma unroll
-            for (int m = 0; m < 2; ++m) st2<false, !LL>(lv[0].p + (long long)((p + m * S) >> 1) * lv[0].s, y[m]);
-        }
-        v[p] = y[(1 << F) - 2].x;
-        v[p + 1] = y[(1 << F) - 2].y;
-        sched_fence();
-    }
-}
-
-// root: 0 = compact source level, RR = root (1 plain, 2 non-temporal loads)
-// NS: non-temporal access to the upper stage levels (all but level D-1)
-template <int F, int G, int RR, bool NS, bool YL>
-PCUB_HD void dispatch_pass(const Chain& c, int La, const LevelMap& lm, int a, bool fg, bool root) {
-    if (root) {
-        if (fg) chain_pass<F, true, RR, G, NS, YL>(c, La, lm, a);
-        else chain_pass<F, false, RR, G, NS, YL>(c, La, lm, a);
-    } else {
-        if (fg) chain_pass<F, true, 0, G, NS, YL>(c, La, lm, a);
-        else chain_pass<F, false, 0, G, NS, YL>(c, La, lm, a);
-    }
-}
-
-template <int S, int F, int G, int RR, bool NS, bool LL, bool YL>
-PCUB_HD void dispatch_final(const Chain& c, const Lvl* lv, double* v, bool fg, bool root) {
-    if (root) {
-        if (fg) chain_final<S, F, true, RR, G, NS, LL, YL>(c, lv, v);
-        else chain_final<S, F, false, RR, G, NS, LL, YL>(c, lv, v);
-    } else {
-        if (fg) chain_final<S, F, true, 0, G, NS, LL, YL>(c, lv, v);
-        else chain_final<S, F, false, 0, G, NS, LL, YL>(c, lv, v);
-    }
-}
-
-// Split of a T-level chain into passes.  Each pass reads only its source level,
-// and levels halve at every depth, so passes are fused greedily from the top
-// (three levels each) and the final pass into registers (one or two levels)
-// takes the remainder: T = 3 -> 2 + 1, 4 -> 3 + 1, 5 -> 3 + 2, 6 -> 3 + 2 + 1.
-// With the deepest stage level in LDS (stored only by a final pass) the final
-// pass is two levels whenever T >= 2.
-template <bool LDS>
-PCUB_HD int final_levels(int T) {
-    if constexpr (LDS) return T >= 2 ? 2 : 1;
-    return (T % 3 == 2) ? 2 : 1;
-}
-
-// Decode codeword `cw` (clamped to a valid index for loads) with lane j of its
-// G lanes (`lane` = wave lane id, for the exchanges) in scratch slot `slot`.
-// S = virtual register subtree (values per lane) in {8, 16, 32}; requires
-// N >= 2*S*G and N >= 32*G.  `store` is false for padding codewords.
-//
 // A register subtree's u decisions and frozen bits live in NW 64-bit windows
 // (NW = S*G/64 when the subtree has more than 64 real positions): WinTree splits
 // the subtree at its top nodes until each part is one window.
@@ -520,218 +388,6 @@ struct WinTree {
         }
     }
 };
-
-template <int S, int G>
-struct SubWin {
-    static constexpr int SU = S * G;
-    static constexpr int NW = SU > 64 ? SU / 64 : 1;
-    static constexpr int SUW = SU > 64 ? 64 : SU;  // bits per window
-    static constexpr uint64_t WMASK = (SUW == 64) ? ~0ull : ((1ull << SUW) - 1ull);
-    static_assert(SU <= 512, "at most eight windows");
-
-    // decisions of the subtree from its S level-D values
-    static PCUB_HD uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm, const uint64_t* fv, int lane) {
-        return WinTree<S, G, NW>::run(v, ub, fm, fv, lane);
-    }
-
-    static PCUB_HD uint32_t frozen(uint64_t* ub, const uint64_t* fv, int j) { return WinTree<S, G, NW>::frozen(ub, fv, j); }
-};
-
-// NT: 0 = cached loads/stores, 1 = non-temporal input rows, 2 = also the upper stage levels
-// YL: the re-encoded bits in LDS (ylds = this thread's column, word w at ylds[w * ystride])
-template <int S, int G, bool LDS = false, int NT = 0, bool YL = false>
-PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
-                             Lvl last = Lvl{nullptr, 0}, uint32_t* ylds = nullptr, long long ystride = 0) {
-    static_assert(S == 8 || S == 16 || S == 32, "register subtree must fit one Y word");
-    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per codeword");
-    constexpr int s = (S == 8) ? 3 : (S == 16) ? 4 : 5;
-    constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : (G == 4) ? 2 : (G == 8) ? 3 : 4;
-    constexpr uint32_t SMASK = (S == 32) ? 0xffffffffu : ((1u << S) - 1u);
-    constexpr int SU = S * G;  // real u positions per register subtree (<= 128)
-    using W = SubWin<S, G>;
-    constexpr int NW = W::NW;
-    constexpr int RR = NT >= 1 ? 2 : 1;
-    constexpr bool NS = NT >= 2;
-    const int n = A.n;
-    const int nv = n - g;
-    const int Nv = 1 << nv;
-    const int D = nv - s;
-    const long long ns = A.nslots;
-    const long long B = A.B;
-    const double2* in = A.xy + cw + 2 * (long long)bitrev((uint32_t)j, n - 1) * B;
-    double2* scr = A.scratch + slot;
-    uint32_t* Y = YL ? ylds : A.ybits + slot;
-    const long long ys = YL ? ystride : ns;  // Y word stride
-
-    // stored levels 1 .. D-2 in the slot scratch; level D-1 there too, or in LDS (`last`)
-    LevelMap lm;
-    lm.scr = scr;
-    lm.ns = ns;
-    lm.Nv = Nv;
-    lm.D = D;
-    lm.last = Lvl{nullptr, 0};
-    Lvl lastlv;
-    if constexpr (LDS) lastlv = last;
-    else lastlv = lm.get(D - 1);
-
-    uint64_t acc = 0;
-    int nacc = 0;
-    int infow = 0;
-
-    for (int k = 0; k < (1 << D); ++k) {
-        in = launder(in);
-        scr = launder(scr);
-        if constexpr (!YL) Y = launder(Y);
-        lm.scr = scr;
-        if constexpr (!LDS) lastlv = lm.get(D - 1);
-        // The chain for subtree k: a plus transform at depth d0-1 (minus for k == 0)
-        // then minus transforms down to depth D.  Passes of up to 3 fused levels;
-        // the last pass (1 or 2 levels) ends in registers.  Only a pass's source
-        // level is read from memory: every level written inside a chain is
-        // consumed from registers by the next transform.
-        const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
-        const int e0 = A.ef[k];  // first rate-0 depth on this chain (D + 1: none)
-        int a = d0 - 1;
-        bool fg = (k != 0);
-        Chain c;
-        c.in = in;
-        c.B = B;
-        c.nv = nv;
-        c.Y = Y;
-        c.ns = ys;
-        // frozen bits of real u range [k*SU, (k+1)*SU), in NW windows
-        uint64_t fm[NW], fv[NW], ub[NW];
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const int us = k * SU + 64 * w;
-            const int uw = us >> 5, ush = us & 31;
-            if constexpr (W::SUW == 64) {
-                fm[w] = (uint64_t)A.fmask[uw] | ((uint64_t)A.fmask[uw + 1] << 32);
-                fv[w] = (uint64_t)A.fval[uw] | ((uint64_t)A.fval[uw + 1] << 32);
-            } else {
-                fm[w] = (uint64_t)((A.fmask[uw] >> ush) & (uint32_t)W::WMASK);
-                fv[w] = (uint64_t)((A.fval[uw] >> ush) & (uint32_t)W::WMASK);
-            }
-            ub[w] = 0;
-        }
-        uint32_t y;
-        if (e0 <= D - 1) {
-            // the chain enters a rate-0 node above the register level: evaluate
-            // (and store, for the plus children to come) only depths d0 .. e0-1
-            int T = e0 - 1 - a;
-            while (T > 0) {
-                const int F = T >= 3 ? 3 : T;
-                c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
-                c.ystart = (k >> (D - a)) << (nv - a);
-                const int La = Nv >> a;
-                if (F == 3) dispatch_pass<3, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
-                else if (F == 2) dispatch_pass<2, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
-                else dispatch_pass<1, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
-                a += F;
-                T -= F;
-                fg = false;
-            }
-            y = W::frozen(ub, fv, j) & SMASK;
-        } else {
-        int T = D - a;
-        const int Ffin = final_levels<LDS>(T);
-        while (T > Ffin) {
-            const int F = (T - Ffin) >= 3 ? 3 : (T - Ffin);
-            c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
-            c.ystart = (k >> (D - a)) << (nv - a);
-            const int La = Nv >> a;
-            if (F == 3) dispatch_pass<3, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
-            else if (F == 2) dispatch_pass<2, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
-            else dispatch_pass<1, G, RR, NS, YL>(c, La, lm, a, fg, a == 0);
-            a += F;
-            T -= F;
-            fg = false;
-        }
-        double v[S];
-        c.ystart = (k >> (D - a)) << (nv - a);
-        if (Ffin == 2) {
-            c.src = a > 0 ? lm.get(a) : Lvl{nullptr, 0};
-            dispatch_final<S, 2, G, RR, NS, LDS, YL>(c, &lastlv, v, fg, a == 0);
-        } else if (a > 0) {
-            c.src = lastlv;
-            dispatch_final<S, 1, G, RR, NS, LDS, YL>(c, &lastlv, v, fg, false);
-        } else {
-            dispatch_final<S, 1, G, RR, NS, LDS, YL>(c, &lastlv, v, fg, true);
-        }
-        if (e0 == D) {  // the register subtree itself is rate-0 (its level-D values go unused)
-            y = W::frozen(ub, fv, j) & SMASK;
-        } else {
-            y = W::run(v, ub, fm, fv, lane) & SMASK;
-        }
-        }
-        // local encoding bits of virtual subtree k
-        const int lstart = k * S;
-        uint32_t* yw = Y + (long long)(lstart >> 5) * ys;
-        if (S == 32) sty<YL>(yw, y);
-        else sty<YL>(yw, ((lstart & 31) == 0 ? 0u : (ldy<YL>(yw) & ((1u << (lstart & 31)) - 1u))) | (y << (lstart & 31)));
-        if (A.uout && store && j == 0) {
-#pragma unroll
-            for (int w = 0; w < NW; ++w) {
-                const int us = k * SU + 64 * w;
-                const int ush = us & 31;
-                uint32_t* uo = A.uout + (long long)(us >> 5) * B + cw;
-                if constexpr (W::SUW == 64) {
-                    uo[0] = (uint32_t)ub[w];
-                    uo[B] = (uint32_t)(ub[w] >> 32);
-                } else if constexpr (W::SUW == 32) {
-                    *uo = (uint32_t)ub[w];
-                } else {
-                    *uo = (ush == 0 ? 0u : (*uo & ((1u << ush) - 1u))) | ((uint32_t)ub[w] << ush);
-                }
-            }
-        }
-        // information bits of this subtree, in u order (identical in all G lanes)
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            for (uint64_t im = ~fm[w] & W::WMASK; im != 0ull; im &= im - 1ull) {
-                const int q = __builtin_ctzll(im);
-                acc |= ((ub[w] >> q) & 1ull) << nacc;
-                if (++nacc == 32) {
-                    if (store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
-                    acc = 0;
-                    nacc = 0;
-                    ++infow;
-                }
-            }
-        }
-        // combine completed plus children upward: parent = [left ^ right | right]
-        for (int d = D; d >= 1 && ((k >> (D - d)) & 1); --d) {
-            const int Lc = Nv >> d;
-            if (Lc < 32) {  // parent fits in one word (S < 32, deepest levels)
-                const int pstart = (k >> (D - d + 1)) * 2 * Lc;
-                uint32_t* pw = Y + (long long)(pstart >> 5) * ys;
-                const uint32_t w0 = ldy<YL>(pw);
-                const uint32_t w = w0 >> (pstart & 31);
-                const uint32_t lm = (1u << Lc) - 1u;
-                sty<YL>(pw, w0 ^ (((w >> Lc) & lm) << (pstart & 31)));
-                continue;
-            }
-            const int Wc = Lc >> 5;
-            uint32_t* base = Y + (long long)((k >> (D - d + 1)) * (2 * Wc)) * ys;
-            for (int w = 0; w < Wc; ++w)
-                sty<YL>(base + (long long)w * ys, ldy<YL>(base + (long long)w * ys) ^ ldy<YL>(base + (long long)(w + Wc) * ys));
-        }
-    }
-    if (nacc && store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
-    // x_hat natural segment k = bitrev_g(j) is this lane's local Y, bit-reversed over nv bits
-    if (A.xhat && store) {
-        const int seg = (int)bitrev((uint32_t)j, g);
-        const int W = Nv >> 5;
-        for (int w = 0; w < W; ++w) {
-            uint32_t o = 0;
-            for (int t = 0; t < 32; ++t) {
-                const uint32_t p = bitrev((uint32_t)(32 * w + t), nv);
-                o |= ((ldy<YL>(Y + (long long)(p >> 5) * ys) >> (p & 31u)) & 1u) << t;
-            }
-            A.xhat[(long long)(seg * W + w) * B + cw] = o;
-        }
-    }
-}
 
 // Small codes (N <= 32): everything in registers, one lane per codeword.
 template <int NN>

@@ -5,7 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include "sc_bin_body.h"
+#include "sc_bin_sched.h"
 
 namespace pcub {
 
@@ -17,10 +17,12 @@ constexpr int kBinBlock = 256;
 // W = minimum waves/SIMD for register allocation, L = deepest stage level in
 // LDS, T = non-temporal loads for the (once-streamed) input rows, Y = the re-encoded bits
 // in LDS (Nv/32 words per thread; only where W workgroups still fit a CU's LDS).
+// H = the chain's last level has 2S values per lane, the first S in LDS (HL; hl_run).
+// P = prefetch distance of the final passes, in column pairs (chain_final).
 struct Variant {
-    int S, G, W, L, T, Y;
+    int S, G, W, L, T, Y, H, P;
 };
-constexpr int kNumVariants = 26;
+constexpr int kNumVariants = 30;
 constexpr Variant kVar[kNumVariants] = {
     {16, 1, 2, 0, 0}, {8, 1, 4, 0, 0}, {32, 1, 1, 0, 0}, {16, 4, 2, 0, 0}, {8, 4, 4, 0, 0}, {16, 2, 2, 0, 0},
     {32, 2, 1, 0, 0}, {8, 8, 4, 0, 0}, {16, 2, 2, 0, 1}, {8, 8, 4, 0, 1}, {16, 4, 2, 0, 1}, {8, 4, 4, 1, 0},
@@ -28,19 +30,29 @@ constexpr Variant kVar[kNumVariants] = {
     {32, 4, 3, 0, 1}, {32, 2, 3, 0, 1}, {32, 8, 2, 0, 1}, {32, 8, 3, 0, 1},
     {32, 16, 2, 0, 1}, {32, 16, 3, 0, 1}, {16, 16, 3, 0, 1},
     {32, 4, 3, 0, 1, 1}, {32, 8, 3, 0, 1, 1},
+    {32, 4, 2, 0, 1, 1, 1, 2}, {32, 4, 2, 0, 1, 1, 1, 1}, {32, 4, 2, 0, 1, 1, 1, 3}, {32, 4, 3, 0, 1, 1, 0, 2},
 };
 
-inline size_t bin_lds_bytes(int v) { return kVar[v].L ? (size_t)kVar[v].S * kBinBlock * sizeof(double2) : 0; }
+// LDS bytes of the stage level (L: S pairs per thread) or of the split level's LDS half (H: S doubles)
+inline size_t bin_lds_bytes(int v) {
+    if (kVar[v].H) return (size_t)kVar[v].S * kBinBlock * sizeof(double);
+    return kVar[v].L ? (size_t)kVar[v].S * kBinBlock * sizeof(double2) : 0;
+}
+
+// values per lane at the end of a chain (the register level; 2S for the split-level variants)
+inline int bin_sr(int v) { return kVar[v].S << kVar[v].H; }
 
 // LDS bytes of the re-encoded bits of variant v at code length 2^n (0 unless Y)
 inline size_t bin_ylds_bytes(int v, int n) {
     return kVar[v].Y ? (size_t)kBinBlock * (((size_t)1 << n) / kVar[v].G / 32) * sizeof(uint32_t) : 0;
 }
 
-template <int S, int G, int W, bool LDS, int NT, bool YL = false>
+template <int S, int G, int W, bool LDS, int NT, bool YL = false, bool HL = false, int PF = 0>
 __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
-    // [S pairs][kBinBlock] when LDS, then [Nv/32 words][kBinBlock] when YL (plus occupancy padding)
+    // [S pairs][kBinBlock] when LDS (HL: [S doubles][kBinBlock]), then [Nv/32 words][kBinBlock]
+    // when YL (plus occupancy padding)
     extern __shared__ double2 lds_last[];
+    constexpr int LDS2 = LDS ? S * kBinBlock : HL ? S / 2 * kBinBlock : 0;  // double2 units before Y
     constexpr int CWB = kBinBlock / G;  // codewords per workgroup tile
     const long long slot = (long long)blockIdx.x * kBinBlock + threadIdx.x;
     const int j = threadIdx.x & (G - 1);
@@ -50,9 +62,9 @@ __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_codeword<S, G, LDS, NT, YL>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last,
-                                           YL ? (uint32_t*)(lds_last + (LDS ? S * kBinBlock : 0)) + threadIdx.x : nullptr,
-                                           kBinBlock);
+        decode_codeword<S, G, LDS, NT, YL, HL, PF>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last,
+                                               YL ? (uint32_t*)(lds_last + LDS2) + threadIdx.x : nullptr, kBinBlock,
+                                               HL ? (double*)lds_last + threadIdx.x : nullptr);
     }
 }
 
@@ -63,5 +75,6 @@ BinKernFn bin_kernel_part0(int v);
 BinKernFn bin_kernel_part1(int v);
 BinKernFn bin_kernel_part2(int v);
 BinKernFn bin_kernel_part3(int v);
+BinKernFn bin_kernel_part4(int v);
 
 }  // namespace pcub

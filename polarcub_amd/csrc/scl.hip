@@ -3,7 +3,10 @@
 //
 // Each lane walks the (frozen-mask-determined) recursion of its codeword with its list of up to
 // L paths in a per-slot slab (slot-minor, so the lanes of a wave, all at the same point of the
-// same recursion, touch consecutive words).  List decoding is a host-side tool in the reference
+// same recursion, touch consecutive words).  The recursion is a loop over an explicit frame
+// stack (scl_run), so the kernel has a fixed private segment and no dynamic stack: the launch
+// never depends on the device's per-thread stack limit, and the library never changes it.
+// List decoding is a host-side tool in the reference
 // (the IR simulation); the kernel batches it, it is not the SC throughput path.
 #include <hip/hip_runtime.h>
 
@@ -40,20 +43,6 @@ long long scl_grid(long long B) {
     return ntiles < g ? ntiles : g;
 }
 
-// SclNode::run recurses (a dynamic stack): at most log2N + 2 nested frames (400 B each in the
-// gfx950 build) above the kernel's own 720 B.  The runtime's default per-thread stack does not
-// cover N = 256 (an illegal-address fault at the bench's shape), so the launcher raises the
-// device's limit to a 1 KiB-per-frame bound when it is lower.
-size_t scl_stack_bytes(int32_t log2N) { return 1024 + (size_t)(log2N + 2) * 1024; }
-
-hipError_t scl_ensure_stack(int32_t log2N) {
-    size_t cur = 0;
-    hipError_t e = hipDeviceGetLimit(&cur, hipLimitStackSize);
-    if (e != hipSuccess) return e;
-    const size_t need = scl_stack_bytes(log2N);
-    return cur >= need ? hipSuccess : hipDeviceSetLimit(hipLimitStackSize, need);
-}
-
 size_t scl_slot_bytes(int32_t q, int32_t log2N, int32_t L, int32_t K) {
     SclLayout Y;
     Y.init(log2N, q, L, K);
@@ -61,12 +50,6 @@ size_t scl_slot_bytes(int32_t q, int32_t log2N, int32_t L, int32_t K) {
 }
 
 }  // namespace
-
-// Diagnostic hook (not part of the stable ABI): the device's per-thread stack limit in bytes.
-extern "C" long long pcub_scl_stack_limit(void) {
-    size_t cur = 0;
-    return hipDeviceGetLimit(&cur, hipLimitStackSize) == hipSuccess ? (long long)cur : -1;
-}
 
 extern "C" size_t pcub_scl_qary_workspace(int64_t B, int32_t q, int32_t log2N, int32_t L, int32_t K) {
     if (B <= 0 || !scl_args_ok(B, q, log2N, L, K)) return 0;
@@ -86,7 +69,6 @@ extern "C" int pcub_scl_qary(const double* xy, int64_t B, int32_t q, int32_t log
     const size_t per_block = (size_t)kSclBlock * scl_slot_bytes(q, log2N, L, K);
     if ((size_t)g * per_block > workspace_bytes) g = (long long)(workspace_bytes / per_block);
     if (g <= 0) return PCUB_EINVAL;
-    if (hipError_t e = scl_ensure_stack(log2N); e != hipSuccess) return (int)e;
     SclLayout Y;
     Y.init(log2N, q, L, K);
     SclArgs A;

@@ -263,19 +263,22 @@ PCUB_HD double scl_prod_enc(SclCtx& c, int d, int slot, int S, long long e) {
     return p;
 }
 
-struct SclNode {
-    // Decode the node at depth d covering u indices [u0, u0 + N >> d), information index ii,
-    // from the Lin input paths (their vectors at depth d, slots 0..Lin-1).  Writes the output
-    // encodings at enc(d, side, r, .) and the map (output path -> input path) at c_map + d*L;
-    // returns the output list size.
-    static PCUB_HD int run(SclCtx& c, int d, int u0, int ii, int side, int Lin) {
-        const SclLayout& Y = c.Y;
-        const int q = Y.q, L = Y.L, S = Y.N >> d;
-        const long long mapo = Y.c_map + (long long)d * L;
-        int nin = 0;
-        for (int j = 0; j < S; ++j) nin += c.A->frozen[u0 + j] == 0;
-        int origin[64];
+// Number of information indices among u0 .. u0 + S - 1.
+PCUB_HD int scl_nin(const SclCtx& c, int u0, int S) {
+    int nin = 0;
+    for (int j = 0; j < S; ++j) nin += c.A->frozen[u0 + j] == 0;
+    return nin;
+}
 
+// A node the reference decodes without recursing (:424-682): information / frozen leaf, rate-0,
+// repetition, rate-1, single parity check.  Decodes the node at depth d covering u indices
+// [u0, u0 + N >> d), information index ii, from the Lin input paths (their vectors at depth d,
+// slots 0..Lin-1); writes the output encodings at enc(d, side, r, .) and the map (output path
+// -> input path) at c_map + d*L; returns the output list size.
+PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int nin, int* origin) {
+    const SclLayout& Y = c.Y;
+    const int q = Y.q, L = Y.L, S = Y.N >> d;
+    const long long mapo = Y.c_map + (long long)d * L;
         if (S == 1) {
             if (nin == 1) {  // information leaf: q forks per path
                 for (int i = 0; i < Lin; ++i) {
@@ -450,65 +453,122 @@ struct SclNode {
             return k;
         }
 
-        // general node
-        const int H = S / 2;
-        const int P = c.track ? L + 1 : L;
-        auto minus = [&](int slot_in, int slot_out) {
-            for (int h = 0; h < H; ++h) {
-                double o[8];
-                for (int u = 0; u < q; ++u) o[u] = 0.0;
-                for (int x1 = 0; x1 < q; ++x1)
-                    for (int x2 = 0; x2 < q; ++x2) {
-                        const int u = (x1 + x2) % q;
-                        o[u] = o[u] + c.row(d, slot_in, 2 * h, x1) * c.row(d, slot_in, 2 * h + 1, x2);
-                    }
-                double t = 0.0;
-                for (int u = 0; u < q; ++u) t = t + o[u];
-                for (int u = 0; u < q; ++u) c.C(Y.dist(d + 1, slot_out, h, u)) = t != 0.0 ? o[u] / t : o[u];
+    return -1;  // not reached: the caller sends only special nodes here
+}
+
+PCUB_HD bool scl_is_special(int S, int nin) { return S == 1 || nin <= 1 || nin >= S - 1; }
+
+// General node, before its minus child (:684-700): the minus transform + sum-normalise of every
+// path's vector (and the actual path's) into depth d + 1.
+PCUB_HD void scl_minus(SclCtx& c, int d, int slot_in, int slot_out) {
+    const SclLayout& Y = c.Y;
+    const int q = Y.q, H = (Y.N >> d) / 2;
+    for (int h = 0; h < H; ++h) {
+        double o[8];
+        for (int u = 0; u < q; ++u) o[u] = 0.0;
+        for (int x1 = 0; x1 < q; ++x1)
+            for (int x2 = 0; x2 < q; ++x2) {
+                const int u = (x1 + x2) % q;
+                o[u] = o[u] + c.row(d, slot_in, 2 * h, x1) * c.row(d, slot_in, 2 * h + 1, x2);
             }
-        };
-        auto plus = [&](int slot_in, int slot_out, long long encm) {
-            for (int h = 0; h < H; ++h) {
-                const int u1 = c.Bt(encm + h);
-                double o[8];
-                for (int u2 = 0; u2 < q; ++u2)
-                    o[u2] = 0.0 + c.row(d, slot_in, 2 * h, (u1 + u2) % q) * c.row(d, slot_in, 2 * h + 1, (q - u2) % q);
-                double t = 0.0;
-                for (int u = 0; u < q; ++u) t = t + o[u];
-                for (int u = 0; u < q; ++u) c.C(Y.dist(d + 1, slot_out, h, u)) = t != 0.0 ? o[u] / t : o[u];
-            }
-        };
-        for (int i = 0; i < Lin; ++i) minus(d == 0 ? 0 : i, i);
-        if (c.track) minus(d == 0 ? 0 : L, L);
-        (void)P;
-        const int Lm = run(c, d + 1, u0, ii, 0, Lin);
-        const long long save = Y.c_save + (long long)d * L;
-        const long long mapm = Y.c_map + (long long)(d + 1) * L;
-        for (int r = 0; r < Lm; ++r) c.C(save + r) = c.C(mapm + r);
-        int iim = ii;
-        for (int j = 0; j < H; ++j) iim += c.A->frozen[u0 + j] == 0;
-        for (int r = 0; r < Lm; ++r) plus(d == 0 ? 0 : (int)c.C(save + r), r, Y.enc(d + 1, 0, r, 0));
-        if (c.track) plus(d == 0 ? 0 : L, L, Y.enc(d + 1, 0, L, 0));
-        const int Lp = run(c, d + 1, u0 + H, iim, 1, Lm);
-        for (int r = 0; r < Lp; ++r) {
-            const int mi = (int)c.C(mapm + r);
-            for (int h = 0; h < H; ++h) {
-                const int xm = c.Bt(Y.enc(d + 1, 0, mi, h)), xp = c.Bt(Y.enc(d + 1, 1, r, h));
-                c.Bt(Y.enc(d, side, r, 2 * h)) = (uint8_t)((xm + xp) % q);
-                c.Bt(Y.enc(d, side, r, 2 * h + 1)) = (uint8_t)((q - xp) % q);
-            }
-            origin[r] = (int)c.C(save + mi);
-        }
-        for (int r = 0; r < Lp; ++r) c.C(mapo + r) = (double)origin[r];
-        if (c.track)
-            for (int h = 0; h < H; ++h) {
-                const int xm = c.Bt(Y.enc(d + 1, 0, L, h)), xp = c.Bt(Y.enc(d + 1, 1, L, h));
-                c.Bt(Y.enc(d, side, L, 2 * h)) = (uint8_t)((xm + xp) % q);
-                c.Bt(Y.enc(d, side, L, 2 * h + 1)) = (uint8_t)((q - xp) % q);
-            }
-        return Lp;
+        double t = 0.0;
+        for (int u = 0; u < q; ++u) t = t + o[u];
+        for (int u = 0; u < q; ++u) c.C(Y.dist(d + 1, slot_out, h, u)) = t != 0.0 ? o[u] / t : o[u];
     }
+}
+
+// General node, between its children (:701-730): the plus transform of a surviving path from
+// its parent's vector given the minus child's encoding at encm.
+PCUB_HD void scl_plus(SclCtx& c, int d, int slot_in, int slot_out, long long encm) {
+    const SclLayout& Y = c.Y;
+    const int q = Y.q, H = (Y.N >> d) / 2;
+    for (int h = 0; h < H; ++h) {
+        const int u1 = c.Bt(encm + h);
+        double o[8];
+        for (int u2 = 0; u2 < q; ++u2)
+            o[u2] = 0.0 + c.row(d, slot_in, 2 * h, (u1 + u2) % q) * c.row(d, slot_in, 2 * h + 1, (q - u2) % q);
+        double t = 0.0;
+        for (int u = 0; u < q; ++u) t = t + o[u];
+        for (int u = 0; u < q; ++u) c.C(Y.dist(d + 1, slot_out, h, u)) = t != 0.0 ? o[u] / t : o[u];
+    }
+}
+
+// General node, after its plus child returned Lp paths (:731-757): combine x[2h] = xm + xp,
+// x[2h+1] = -xp (mod q) from each output path's minus-side ancestor, and compose the maps.
+PCUB_HD void scl_combine(SclCtx& c, int d, int side, int Lp, int* origin) {
+    const SclLayout& Y = c.Y;
+    const int q = Y.q, L = Y.L, H = (Y.N >> d) / 2;
+    const long long mapo = Y.c_map + (long long)d * L;
+    const long long save = Y.c_save + (long long)d * L;
+    const long long mapm = Y.c_map + (long long)(d + 1) * L;
+    for (int r = 0; r < Lp; ++r) {
+        const int mi = (int)c.C(mapm + r);
+        for (int h = 0; h < H; ++h) {
+            const int xm = c.Bt(Y.enc(d + 1, 0, mi, h)), xp = c.Bt(Y.enc(d + 1, 1, r, h));
+            c.Bt(Y.enc(d, side, r, 2 * h)) = (uint8_t)((xm + xp) % q);
+            c.Bt(Y.enc(d, side, r, 2 * h + 1)) = (uint8_t)((q - xp) % q);
+        }
+        origin[r] = (int)c.C(save + mi);
+    }
+    for (int r = 0; r < Lp; ++r) c.C(mapo + r) = (double)origin[r];
+    if (c.track)
+        for (int h = 0; h < H; ++h) {
+            const int xm = c.Bt(Y.enc(d + 1, 0, L, h)), xp = c.Bt(Y.enc(d + 1, 1, L, h));
+            c.Bt(Y.enc(d, side, L, 2 * h)) = (uint8_t)((xm + xp) % q);
+            c.Bt(Y.enc(d, side, L, 2 * h + 1)) = (uint8_t)((q - xp) % q);
+        }
+}
+
+// The recursion of recursiveListDecode (:403-757) as a loop over an explicit frame stack (one
+// frame per depth, at most log2 N + 1 live): no device function calls itself, so the kernel has
+// a fixed private segment and no dynamic stack (scripts/check_isa.py rejects one).  A frame's
+// phase says which child it waits for.  Returns the final list size.
+constexpr int kSclMaxDepth = 13;  // log2 N <= 12
+
+struct SclFrame {
+    int d, u0, ii, side, Lin, phase;
 };
+
+PCUB_HD int scl_run(SclCtx& c) {
+    const SclLayout& Y = c.Y;
+    const int L = Y.L;
+    SclFrame st[kSclMaxDepth];
+    int origin[64];
+    int sp = 0, ret = 0;
+    st[0] = SclFrame{0, 0, 0, 0, 1, 0};
+    while (sp >= 0) {
+        SclFrame& f = st[sp];
+        const int S = Y.N >> f.d, H = S / 2;
+        if (f.phase == 0) {
+            const int nin = scl_nin(c, f.u0, S);
+            if (scl_is_special(S, nin)) {
+                ret = scl_special(c, f.d, f.u0, f.ii, f.side, f.Lin, nin, origin);
+                --sp;
+                continue;
+            }
+            for (int i = 0; i < f.Lin; ++i) scl_minus(c, f.d, f.d == 0 ? 0 : i, i);
+            if (c.track) scl_minus(c, f.d, f.d == 0 ? 0 : L, L);
+            f.phase = 1;
+            st[sp + 1] = SclFrame{f.d + 1, f.u0, f.ii, 0, f.Lin, 0};
+            ++sp;
+        } else if (f.phase == 1) {
+            const int Lm = ret;
+            const long long save = Y.c_save + (long long)f.d * L;
+            const long long mapm = Y.c_map + (long long)(f.d + 1) * L;
+            for (int r = 0; r < Lm; ++r) c.C(save + r) = c.C(mapm + r);
+            const int iim = f.ii + scl_nin(c, f.u0, H);
+            for (int r = 0; r < Lm; ++r) scl_plus(c, f.d, f.d == 0 ? 0 : (int)c.C(save + r), r, Y.enc(f.d + 1, 0, r, 0));
+            if (c.track) scl_plus(c, f.d, f.d == 0 ? 0 : L, L, Y.enc(f.d + 1, 0, L, 0));
+            f.phase = 2;
+            st[sp + 1] = SclFrame{f.d + 1, f.u0 + H, iim, 1, Lm, 0};
+            ++sp;
+        } else {
+            scl_combine(c, f.d, f.side, ret, origin);  // ret = the plus child's list size = this node's
+            --sp;
+        }
+    }
+    return ret;
+}
 
 // decode codeword cw with slab slot `slot`; store = false for padding lanes
 PCUB_HD void scl_decode_cw(const SclArgs& A, long long cw, long long slot, bool store) {
@@ -524,7 +584,7 @@ PCUB_HD void scl_decode_cw(const SclArgs& A, long long cw, long long slot, bool 
     c.track = A.actual != nullptr;
     c.actual_prob = 1.0;
     c.C(c.Y.c_prob) = 1.0;
-    const int k = SclNode::run(c, 0, 0, 0, 0, 1);
+    const int k = scl_run(c);
     if (!store) return;
     const long long B = A.B;
     A.out_size[cw] = k;

@@ -1,3 +1,5 @@
-"""Drop-in alias of polarcub_amd.coding_qary (the reference's QaryPolarEncoderDecoder module, SC part)."""
-from polarcub_amd.coding_qary import (QaryPolarEncoderDecoder, encodeDecodeSimulation,  # noqa: F401
-                                      frozenSetFromTVAndPe, polarTransformOfQudits, uIndexType)
+"""Drop-in alias of polarcub_amd.coding_qary (the reference's QaryPolarEncoderDecoder module)."""
+from polarcub_amd.coding_qary import (ProbResult, QaryPolarEncoderDecoder, calcNormalizationVector,  # noqa: F401
+                                      encodeDecodeSimulation, encodeListDecodeSimulation, frozenSetFromTVAndPe,
+                                      genieEncodeDecodeSimulation, hamming, irSimulation, make_cmp_function,
+                                      normalize, normalizeDistList, polarTransformOfQudits, prefix, uIndexType)

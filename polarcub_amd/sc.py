@@ -112,6 +112,12 @@ def default_variant():
     return int(_lib.lib().pcub_sc_default_variant())
 
 
+def variant_for(n):
+    """The decode kernel variant a code of length 2^n launches (the selected variant, or the
+    fallback the launcher picks where it does not fit)."""
+    return int(_lib.lib().pcub_sc_variant_for(int(n)))
+
+
 def set_variant(v=None):
     """Select the decode kernel variant (see variants()); None restores the default."""
     if v is None:

@@ -191,6 +191,73 @@ class BinaryMemorylessDistribution:
         return vd
 
 
+use_fast = False  # the reference's switch for its (absent) Cython eta/hxgiveny (:10-14)
+
+
+# The degrade / upgrade merge-cost helpers (:509-621).  The constructions themselves run in the
+# native host library (csrc/host/tv_core.h restates the same arithmetic); these are the
+# reference's Python entry points, for callers that use them directly.
+def _calcKey_degrade(dataLeft, dataCenter):
+    """Cost of merging two adjacent letters (:510-521); data = (probs, ...) tuples as in the
+    reference's heap entries."""
+    if dataLeft is None:
+        return float("inf")
+    probLeft, probCenter = dataLeft[0], dataCenter[0]
+    assert len(probLeft) == len(probCenter) == 2
+    probMerge = [probLeft[0] + probCenter[0], probLeft[1] + probCenter[1]]
+    return hxgiveny(probMerge) - hxgiveny(probLeft) - hxgiveny(probCenter)
+
+
+def _calcKey_upgrade(dataLeft, dataCenter, dataRight):
+    """Cost of splitting the centre letter onto its neighbours (:524-537)."""
+    if dataLeft is None or dataRight is None:
+        return float("inf")
+    assert len(dataLeft[0]) == len(dataCenter[0]) == len(dataRight[0]) == 2
+    probMergeLeft, probMergeRight = upgradedLeftRightProbs(dataLeft, dataCenter, dataRight)
+    return hxgiveny(dataCenter[0]) - hxgiveny(probMergeLeft) - hxgiveny(probMergeRight)
+
+
+def _listIndexingHelper(l, i):
+    return l[i] if (0 <= i < len(l)) else None
+
+
+def upgradedLeftRightProbs(dataLeft, dataCenter, dataRight):
+    """Split of the centre letter's mass pi_c into theta_l * pi_c and theta_r * pi_c along its
+    neighbours' posteriors (:544-621), with the reference's case split for numerical stability
+    (the smaller theta computed directly, the other as 1 - theta)."""
+    probLeft, probCenter, probRight = dataLeft[0], dataCenter[0], dataRight[0]
+    piLeft, piCenter, piRight = sum(probLeft), sum(probCenter), sum(probRight)
+    nL = [probLeft[b] / piLeft for b in range(2)]
+    nC = [probCenter[b] / piCenter for b in range(2)]
+    nR = [probRight[b] / piRight for b in range(2)]
+    if nL[0] < 0.5 and nR[0] < 0.5:
+        dLR = 2.0 * (nL[0] - nR[0])
+    elif nL[1] < 0.5 and nR[1] < 0.5:
+        dLR = 2.0 * (nR[1] - nL[1])
+    else:
+        dLR = (nL[0] - nL[1]) - (nR[0] - nR[1])
+    assert dLR > 0.0  # equivalent letters are merged before upgrading
+    if nL[0] < 0.5 and nR[0] < 0.5:
+        if nL[0] - nC[0] < nC[0] - nR[0]:
+            thetaRight = 2.0 * (nL[0] - nC[0]) / dLR
+            thetaLeft = 1.0 - thetaRight
+        else:
+            thetaLeft = 2.0 * (nC[0] - nR[0]) / dLR
+            thetaRight = 1.0 - thetaLeft
+    elif nL[1] < 0.5 and nR[1] < 0.5:
+        if nC[1] - nL[1] < nR[1] - nC[1]:
+            thetaRight = 2.0 * (nC[1] - nL[1]) / dLR
+            thetaLeft = 1.0 - thetaRight
+        else:
+            thetaLeft = 2.0 * (nR[1] - nC[1]) / dLR
+            thetaRight = 1.0 - thetaLeft
+    else:
+        thetaRight = ((nL[0] - nL[1]) - (nC[0] - nC[1])) / dLR
+        thetaLeft = 1.0 - thetaRight
+    assert 0.0 <= thetaLeft <= 1.0 and 0.0 <= thetaRight <= 1.0
+    return ([thetaLeft * piCenter * nL[b] for b in range(2)], [thetaRight * piCenter * nR[b] for b in range(2)])
+
+
 def makeBSC(p):
     bsc = BinaryMemorylessDistribution()
     bsc.append([0.5 * (1.0 - p), 0.5 * p])

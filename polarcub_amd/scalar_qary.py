@@ -13,10 +13,23 @@ calcFrozenSet_degradingUpgrading / calcTVAndPe_degradingUpgrading with its .npy 
 """
 import math
 import os
+from enum import Enum
 
 import numpy as np
 
 from . import construction, vectors
+
+# constants (ScalarDistributions/QaryMemorylessDistribution.py:15-17): the left / centre / right
+# images of an old letter in the dynamic upgrade
+lcrLeft = 0
+lcrCenter = 1
+lcrRight = 2
+
+
+class Binning(Enum):
+    """Cell functions of the static constructions (:20-22)."""
+    TalSharovVardy = 1  # standard cell function for static degrade
+    PeregTal = 2  # standard cell function for static upgrade
 
 
 def eta(p):
@@ -176,6 +189,42 @@ def makeQEC(q, p):
     return qec
 
 
+def makeAWGN(q, snr, rate):
+    """The reference's placeholder (:800-804): binary only, and the channel has no output
+    letters (probs == []); test3.py's AWGN branch builds nothing usable from it."""
+    assert (q == 2)
+    awgn = QaryMemorylessDistribution(q)
+    awgn.probs = []
+    return awgn
+
+
+def makeQuantizedUniform(q, T):
+    """Joint distribution with output (a_0, .., a_{q-1}), a_i >= 0 summing to T, and
+    P(x, a) = a_x / (M T), M = binom(T + q - 1, q - 1) output letters (:815-853); letters in the
+    reference's lexicographic enumeration order."""
+    M = math.comb(T + q - 1, q - 1)
+    quantizedUniform = QaryMemorylessDistribution(q)
+    recursivlyBuildQuantizedUniform(quantizedUniform, [], q, T, M)
+    return quantizedUniform
+
+
+def recursivlyBuildQuantizedUniform(quantizedUniform, outputLetter, level, T, M):
+    """Enumerates the output letters of makeQuantizedUniform (:856-873), appending to
+    quantizedUniform.probs; outputLetter is the prefix built so far."""
+    if level == 0:
+        quantizedUniform.probs.append([(1.0 * outputLetter[x]) / (M * T) for x in range(quantizedUniform.q)])
+        return
+    if level == 1:
+        outputLetter.append(T - sum(outputLetter))
+        recursivlyBuildQuantizedUniform(quantizedUniform, outputLetter, level - 1, T, M)
+        outputLetter.pop()
+        return
+    for t in range(0, T + 1 - sum(outputLetter)):
+        outputLetter.append(t)
+        recursivlyBuildQuantizedUniform(quantizedUniform, outputLetter, level - 1, T, M)
+        outputLetter.pop()
+
+
 def makeInputDistribution(probs):
     dist = QaryMemorylessDistribution(len(probs))
     dist.append(list(probs))
@@ -244,3 +293,16 @@ def upgrade_dynamic_upper_bound(q, L):
     """Equation (13) of Ordentlich-Tal, in bits (:885-891)."""
     M = construction.calc_m(q, L)
     return (128 * (q - 1) / (M ** 2)) / math.log(2)
+
+
+def degrade_cost_lower_bound(q, L):
+    """Equation (3) of Tal, "On the construction of polar codes for channels with moderate
+    input alphabet sizes", in bits (:894-899)."""
+    sigma = (math.pi ** ((q - 1) / 2)) / (math.gamma((q - 1) / 2 + 1))
+    return (q - 1) / (2 * (q + 1)) * ((1.0 / (sigma * math.factorial(q - 1) * L)) ** (2 / (q - 1))) / math.log(2)
+
+
+def upgrade_cost_lower_bound(q, L):
+    """Equation (43) of Kartowsky-Tal, in bits (:902-907)."""
+    kappa = (q - 1) / (2 * math.pi * (q + 1)) * (math.gamma(1 + (q - 1) / 2) / math.factorial(q - 1))
+    return kappa * (L ** (-2 / (q - 1))) / math.log(2)

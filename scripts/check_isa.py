@@ -15,6 +15,13 @@ deletion node functions with lane exchanges gave batch-dependent wrong results o
 (round 2: 32-trellis shapes, the host emulation clean under ASan/UBSan); they are
 force-inlined, and this rule keeps them so.
 
+Third rule: no kernel uses a dynamic stack.  Its code-object metadata
+(`.uses_dynamic_stack`, read with llvm-readelf --notes) must be false: a kernel whose stack
+depth the compiler cannot bound (recursion, e.g. round 2's SclNode::run) overruns each wave's
+scratch at full occupancy unless the device's per-thread stack limit is raised, a device-wide
+side effect a library call must not have.  `--report` prints every kernel's private segment
+size and spill counts as JSON.
+
 Exit status 1 lists the offending functions.
 """
 import os
@@ -67,6 +74,33 @@ def device_disasm(lib):
     return "\n".join(texts)
 
 
+def kernel_metadata(lib):
+    """[{name, uses_dynamic_stack, private_segment_fixed_size, vgpr_count, sgpr_count,
+    vgpr_spill_count, sgpr_spill_count, group_segment_fixed_size}] of every gfx950 kernel (the
+    AMDGPU metadata note of each code object)."""
+    keys = ("uses_dynamic_stack", "private_segment_fixed_size", "vgpr_count", "sgpr_count", "vgpr_spill_count",
+            "sgpr_spill_count", "group_segment_fixed_size")
+    out = []
+    with tempfile.TemporaryDirectory() as d:
+        for i, co in enumerate(code_objects(lib)):
+            f = os.path.join(d, "co%d.o" % i)
+            with open(f, "wb") as fh:
+                fh.write(co)
+            notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", f], check=True,
+                                   capture_output=True, text=True).stdout
+            for block in re.split(r"\n\s*- \.agpr_count:", notes)[1:]:
+                m = re.search(r"^\s*\.name:\s+(\S+)", block, re.M)
+                if not m:
+                    continue
+                k = {"name": m.group(1)}
+                for key in keys:
+                    v = re.search(r"^\s*\.%s:\s+(\S+)" % key, block, re.M)
+                    if v:
+                        k[key] = v.group(1) == "true" if key == "uses_dynamic_stack" else int(v.group(1))
+                out.append(k)
+    return out
+
+
 # device functions allowed to exchange lanes: called by wave 0 of the deletion kernel with all
 # lanes active (the T > 64 window decoder, kept out of line for the branch range above)
 CROSS_LANE_OK = ("del_window",)
@@ -74,9 +108,20 @@ CROSS_LANE = re.compile(r"ds_bpermute|ds_permute|ds_swizzle|quad_perm|row_ror|ro
 
 
 def main():
-    lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "polarcub_amd", "lib", "libpolarcub_hip.so")
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    lib = args[0] if args else os.path.join(ROOT, "polarcub_amd", "lib", "libpolarcub_hip.so")
+    meta = kernel_metadata(lib)
+    if "--report" in sys.argv:
+        import json
+        print(json.dumps(meta, indent=1))
     text = device_disasm(lib)
     bad = []
+    for k in meta:
+        if k.get("uses_dynamic_stack", True):
+            bad.append((k["name"], 1, "dynamic stack (.uses_dynamic_stack, private segment %s B)"
+                        % k.get("private_segment_fixed_size")))
+    if not meta:
+        bad.append(("<library>", 1, "no kernel metadata found"))
     for m in re.finditer(r"^[0-9a-f]+ <([^>]+)>:\n(.*?)(?=^[0-9a-f]+ <|\Z)", text, re.S | re.M):
         name, body = m.group(1), m.group(2)
         if ".kd" in name:
@@ -98,8 +143,9 @@ def main():
         if x and not any(a in name for a in CROSS_LANE_OK):
             bad.append((name, x, "cross-lane operations in an out-of-line device function (%d)" % x))
     for name, n, what in bad:
-        print("%s in device function %s" % (what, name))
-    print("%d function(s) checked, %d hazard(s)" % (len(re.findall(r"^[0-9a-f]+ <", text, re.M)), len(bad)))
+        print("%s in %s" % (what, name))
+    print("%d function(s), %d kernel(s) checked, %d hazard(s)" % (len(re.findall(r"^[0-9a-f]+ <", text, re.M)),
+                                                                  len(meta), len(bad)))
     return 1 if bad else 0
 
 

@@ -6,7 +6,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
-#include "sc_bin_body.h"
+#include "sc_bin_sched.h"
 
 using namespace pcub;
 

@@ -70,3 +70,20 @@ def test_no_long_branch_through_the_return_address():
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 hazard(s)" in r.stdout
+
+
+def test_no_kernel_uses_a_dynamic_stack():
+    """Every kernel's code-object metadata says .uses_dynamic_stack: false (the SCL recursion is
+    an explicit frame loop since round 3; no launcher sets the device's stack limit)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import check_isa
+    from polarcub_amd import build
+    build.build()
+    meta = check_isa.kernel_metadata(build.LIB)
+    assert len(meta) > 50
+    assert [k["name"] for k in meta if k.get("uses_dynamic_stack", True)] == []
+    scl = [k for k in meta if "k_scl" in k["name"]]
+    assert scl and all(k["private_segment_fixed_size"] < 4096 for k in scl)
+    src = open(os.path.join(ROOT, "polarcub_amd", "csrc", "scl.hip")).read()
+    assert "hipDeviceSetLimit" not in src

@@ -87,10 +87,10 @@ def test_list_decode_facade_single_word(sc):
 
 
 def test_gpu_list_decoder_full_occupancy(sc):
-    """A batch that fills every resident workgroup (2^17 codewords, q=4, N=256, L=8): the
-    recursion's dynamic stack must fit each wave's scratch at full occupancy (the runtime's
-    1 KiB default does not; the launcher raises it), and the first codewords decode as they
-    do alone."""
+    """A batch that fills every resident workgroup (2^17 codewords, q=4, N=256, L=8) at the
+    runtime's default per-thread stack limit (the recursion is an explicit frame loop, the kernel
+    has no dynamic stack, and the library no longer raises the limit), and the first codewords
+    decode as they do alone."""
     import torch
     rng = np.random.default_rng(5)
     q, n, L, B = 4, 8, 8, 1 << 17
@@ -99,8 +99,14 @@ def test_gpu_list_decoder_full_occupancy(sc):
     dec = sc.QaryListDecoder(q, N, frozen, L)
     xy = torch.rand((N, B, q), dtype=torch.float64, device="cuda")
     fv = torch.zeros((int(frozen.sum()), B), dtype=torch.uint8, device="cuda")
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    limit = ctypes.c_size_t(0)
+    assert hip.hipDeviceGetLimit(ctypes.byref(limit), 0) == 0  # hipLimitStackSize
+    before = limit.value
     info, prob, size, _ = dec.decode_native(xy, fv)
     torch.cuda.synchronize()
+    assert hip.hipDeviceGetLimit(ctypes.byref(limit), 0) == 0 and limit.value == before
     assert int(size.min()) >= 1
     info1, prob1, size1, _ = dec.decode_native(xy[:, :6].contiguous(), fv[:, :6].contiguous())
     assert torch.equal(size[:6], size1)

@@ -156,6 +156,18 @@ int pcub_scl_qary(const double* xy, int64_t B, int32_t q, int32_t log2N, int32_t
                   double* out_prob, int32_t* out_size, double* out_actual, void* workspace, size_t workspace_bytes,
                   void* stream);
 
+/* The same list decoder in the log domain: QaryPolarEncoderDecoder(..., use_log=True).listDecode,
+ * recursiveListDecode's use_log branches (QaryPolarEncoderDecoder.py:403-757, normalize :867-872).
+ * xy holds log-probabilities; out_prob / out_actual are log-domain metrics (the largest is 0).
+ * Transforms by numpy's logaddexp and scipy's logsumexp as pcub_sc_decode_qary_log, metrics add,
+ * the products of the linear domain become the reference's sums (np.sum's pairwise order over a
+ * node's positions).  exp / log1p / log are the device's: values agree with the reference to a few
+ * ulps.  Same arguments, workspace and tie rules as pcub_scl_qary. */
+int pcub_scl_qary_log(const double* xy, int64_t B, int32_t q, int32_t log2N, int32_t L, const uint8_t* frozen,
+                      const uint8_t* frozen_vals, int32_t nF, const uint8_t* actual, int32_t K, uint8_t* out_info,
+                      double* out_prob, int32_t* out_size, double* out_actual, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
 /* Non-uniform a-priori distribution (two trees).  Replaces recursiveEncodeDecode with an
  * xVectorDistribution that is not uniform (BinaryPolarEncoderDecoder.py:223-325, called by
  * decode :71-99 and encode :46-69): the prior tree px runs beside the xy tree through the same

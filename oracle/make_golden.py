@@ -1031,24 +1031,27 @@ def fx_combine_codes(R, timing):
          out=np.array(out))
 
 
-def fx_scl(R, timing):
+def fx_scl(R, timing, use_log=False):
     """The reference's q-ary list decoder (QaryPolarEncoderDecoder.listDecode / recursiveListDecode,
     :118-227, 403-820) on tie-free inputs (continuous random rows, no zeros), with an actual
     information word: the final list (informationList[:finalListSize], captured from the
     outermost recursiveListDecode return), prob_list, actual_prob and the returned ProbResult.
-    The list ORDER is numpy-argpartition-dependent; tests compare it as a set."""
+    The list ORDER is numpy-argpartition-dependent; tests compare it as a set.
+    use_log=True: the same cases in the log domain (QaryPolarEncoderDecoder(..., use_log=True), rows
+    np.log of the linear ones, log-domain vector distributions) -> scl_log.npz."""
     QPED = R["QPED"]
     rs = np.random.default_rng(404)
+    lg = np.log if use_log else (lambda a: a)
     out, cases = {}, []
     specs = [(2, 3, 2, 0.5), (2, 4, 4, 0.5), (3, 3, 2, 0.4), (3, 4, 4, 0.5), (4, 3, 4, 0.5), (4, 4, 8, 0.5),
              (2, 5, 8, 0.6), (3, 5, 3, 0.5), (4, 5, 4, 0.6), (2, 4, 1, 0.5), (4, 4, 16, 0.3), (3, 3, 8, 0.2)]
     for ci, (q, n, L, fr) in enumerate(specs):
         N = 1 << n
         frozen = set(int(i) for i in np.nonzero(rs.random(N) < fr)[0])
-        dec = QPED.QaryPolarEncoderDecoder(q, N, frozen, 1)
+        dec = QPED.QaryPolarEncoderDecoder(q, N, frozen, 1, use_log=use_log)
         T = 12
         K = dec.k
-        xy = rs.random((T, N, q)) * 0.98 + 0.02
+        xy = lg(rs.random((T, N, q)) * 0.98 + 0.02)
         fv = rs.integers(0, q, (T, len(frozen)))
         act = rs.integers(0, q, (T, K))
         infos = np.full((T, L, K), -1, np.int64)
@@ -1058,7 +1061,7 @@ def fx_scl(R, timing):
         ret = np.zeros((T, K), np.int64)
         pres = []
         for t in range(T):
-            vd = R["QMVD"].QaryMemorylessVectorDistribution(q, N)
+            vd = R["QMVD"].QaryMemorylessVectorDistribution(q, N, use_log=use_log)
             vd.probs[:] = xy[t]
             orig = dec.recursiveListDecode
             depth = [0]
@@ -1106,19 +1109,24 @@ def fx_scl(R, timing):
             return [float(x) + _c.gauss(0.0, _s) for x in a]
 
         def make_xy(b, _q=q, _s=sig, _N=N):
-            vd = R["QMVD"].QaryMemorylessVectorDistribution(_q, _N)
+            vd = R["QMVD"].QaryMemorylessVectorDistribution(_q, _N, use_log=use_log)
             for i, y in enumerate(b):
-                vd.probs[i] = [math.exp(-((y - x) ** 2) / (2 * _s * _s)) for x in range(_q)]
+                if use_log:  # log-likelihood rows
+                    vd.probs[i] = [-((y - x) ** 2) / (2 * _s * _s) for x in range(_q)]
+                else:
+                    vd.probs[i] = [math.exp(-((y - x) ** 2) / (2 * _s * _s)) for x in range(_q)]
             return vd
         np.random.seed(77)
         buf = io.StringIO()
         with contextlib.redirect_stdout(buf):
-            fe, se, rate, prl = QPED.irSimulation(q, N, simulate, make_xy, T, frozen, L, cs, verbosity=1)
+            fe, se, rate, prl = QPED.irSimulation(q, N, simulate, make_xy, T, frozen, L, cs, use_log=use_log,
+                                                  verbosity=1)
         out[name + "_frozen"] = np.array([1 if i in frozen else 0 for i in range(N)], np.uint8)
         irs.append(dict(name=name, q=q, n=n, L=L, trials=T, sigma=sig, check_size=cs, chan_seed=1234 + q,
                         np_seed=77, frame_error_prob=fe, symbol_error_prob=float(se), rate=rate,
                         prob_results=[p.name for p in prl], printed=buf.getvalue()))
-    save("scl", dict(cases=cases, ir=irs, note="listDecode with actualInformation; list order is argpartition's"),
+    save("scl_log" if use_log else "scl", dict(cases=cases, ir=irs, use_log=use_log,
+                                               note="listDecode with actualInformation; list order is argpartition's"),
          **out)
 
 
@@ -1368,6 +1376,65 @@ def fx_test3_body(R, timing):
 
 FIXTURES["harness_names"] = fx_harness_names
 FIXTURES["test3_body"] = fx_test3_body
+
+
+def fx_deletion_genie_wide(R, timing):
+    """The reference's genie construction (genieEncodeDecodeSimulation, BinaryPolarEncoderDecoder.py:390-491)
+    over the deletion channel at shapes past 64 trellises and with guard-band ones
+    (main_deletion.py:122-133 closures, trustXYProbs = n > n0): main_deletion's own default n0 = n//3
+    at n = 10 (128 trellises), n0 = 1 at n = 8 / 9 (128 / 256 trellises), and ones = 1, 2, 3.
+    Records the TV + Pe score vector handed to frozenSetFromTVAndPe and the returned frozen set;
+    plus the reference main_deletion.py itself at -n 10 -g 6 -e 4 (runpy), its printed lines."""
+    import contextlib
+    import io
+    import runpy
+    BPED = R["BPED"]
+    cases = [(10, 3, 0.1, 0, 6), (8, 1, 0.1, 0, 8), (9, 1, 0.05, 0, 4), (8, 2, 0.1, 1, 8), (9, 1, 0.1, 2, 3),
+             (7, 1, 0.2, 3, 8)]
+    out = {}
+    for ci, (n, n0, pd, ones, G) in enumerate(cases):
+        N = 1 << n
+        make_x, make_codeword, channel, make_xy = deletion_closures(R, n, n0, pd, 0.1, ones, 100 + ci)
+        cap = {}
+        orig = BPED.frozenSetFromTVAndPe
+
+        def capture(TV, Pe, bound, _orig=orig):
+            cap["score"] = [float(a) + float(b) for a, b in zip(TV, Pe)]
+            return _orig(TV, Pe, bound)
+
+        BPED.frozenSetFromTVAndPe = capture
+        t0 = time.time()
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                frozen = BPED.genieEncodeDecodeSimulation(N, make_x, make_codeword, channel, make_xy, G, 0.1,
+                                                          genieSeed=300 + ci, trustXYProbs=n <= n0, filename=None)
+        finally:
+            BPED.frozenSetFromTVAndPe = orig
+        print("  genie n=%d n0=%d ones=%d: %d trials, %.1f s" % (n, n0, ones, G, time.time() - t0))
+        out["c%d_score" % ci] = np.array(cap["score"])
+        out["c%d_frozen" % ci] = np.array([1 if i in frozen else 0 for i in range(N)], np.uint8)
+        out["c%d_shape" % ci] = np.array([n, n0, ones, G], np.int32)
+        out["c%d_pd" % ci] = np.array([pd])
+    argv = ["main_deletion.py", "-n", "10", "-g", "6", "-e", "4"]
+    old = sys.argv
+    sys.argv = argv
+    buf = io.StringIO()
+    t0 = time.time()
+    try:
+        with contextlib.redirect_stdout(buf):
+            runpy.run_path(os.path.join(REF, "main_deletion.py"), run_name="__main__")
+    finally:
+        sys.argv = old
+    print("  main_deletion -n 10: %.1f s" % (time.time() - t0))
+    lines = buf.getvalue().strip().splitlines()
+    keep = [l for l in lines if not l.startswith(("TVVec", "pevec", "HEncvec", "HDecvec"))]
+    save("deletion_genie_wide", dict(cases=len(cases), xi=0.1, channel_seed="100 + case", genie_seed="300 + case",
+                                     bound=0.1, note="(n, n0, ones, trials) per case", main_argv=argv[1:],
+                                     main_lines=keep), **out)
+
+
+FIXTURES["deletion_genie_wide"] = fx_deletion_genie_wide
+FIXTURES["scl_log"] = lambda R, t: fx_scl(R, t, use_log=True)
 
 
 def main():

@@ -20,7 +20,8 @@ kernel (pcub_sc_decode_qary_log: numpy's logaddexp and scipy's logsumexp restate
 over the device's exp/log1p/log, so within a few ulps of the reference rather than
 bit-identical).  Other plugins use the generic recursion over the plugin's own
 methods.  List decoding (listDecode, :118-227, 403-820) runs on the GPU list decoder
-(pcub_scl_qary, linear domain) and irSimulation / ir (:822-930) batch it; the list's
+(pcub_scl_qary; pcub_scl_qary_log for use_log=True, within a few ulps of the reference's
+log-domain metrics) and irSimulation / ir (:822-930) batch it; the list's
 tie-breaking and order are documented in include/polarcub_sc.h.
 """
 import math
@@ -139,15 +140,18 @@ class QaryPolarEncoderDecoder:
 
     # -- list decoding and information reconciliation (:118-242, 822-865) --------------------
     def list_decode_batch(self, xy, frozenValues, maxListSize, actualInformation=None):
-        """Batched listDecode core on the GPU (pcub_scl_qary): xy [B, N, q] linear-domain rows,
-        frozenValues [B, nF], actualInformation [B, K] or None -> (info [B, L, K] int64 with -1
-        rows past each list's size, prob [B, L], size [B], actual_prob [B] | None)."""
+        """Batched listDecode core on the GPU (pcub_scl_qary, or pcub_scl_qary_log when use_log):
+        xy [B, N, q] rows in the decoder's domain, frozenValues [B, nF], actualInformation [B, K]
+        or None -> (info [B, L, K] int64 with -1 rows past each list's size, prob [B, L], size [B],
+        actual_prob [B] | None)."""
         from . import sc
         if not hasattr(self, "_scl"):
             self._scl = {}
-        dec = self._scl.get(int(maxListSize))
+        key = (int(maxListSize), bool(self.use_log))
+        dec = self._scl.get(key)
         if dec is None:
-            dec = self._scl[int(maxListSize)] = sc.QaryListDecoder(self.q, self.length, self._mask, int(maxListSize))
+            dec = self._scl[key] = sc.QaryListDecoder(self.q, self.length, self._mask, int(maxListSize),
+                                                      use_log=bool(self.use_log))
         info, prob, size, ap = dec.decode(xy, frozenValues, actualInformation)
         info = info.astype(np.int64)
         info[info == 0xff] = -1
@@ -180,10 +184,9 @@ class QaryPolarEncoderDecoder:
 
     def listDecode(self, xyVectorDistribution, frozenValues, maxListSize, check_matrix, check_value,
                    actualInformation=None, verbosity=0):
-        """QaryPolarEncoderDecoder.listDecode (:118-227) on the GPU list decoder; the list's
-        tie-breaking and order are documented in include/polarcub_sc.h."""
-        if getattr(xyVectorDistribution, "use_log", False) or self.use_log:
-            raise NotImplementedError("list decoding runs in the linear domain only (use_log=False)")
+        """QaryPolarEncoderDecoder.listDecode (:118-227) on the GPU list decoder, linear or log
+        domain (use_log); the list's tie-breaking and order are documented in include/polarcub_sc.h."""
+        self._check_domain(xyVectorDistribution)
         assert len(xyVectorDistribution) == self.length
         xy = np.asarray(xyVectorDistribution.probs, dtype=np.float64)[None]
         act = None if actualInformation is None else np.asarray(actualInformation)[None]
@@ -192,6 +195,14 @@ class QaryPolarEncoderDecoder:
         self.actual_prob = None if ap is None else float(ap[0])
         return self._list_result(info[0], prob[0], int(size[0]), self.actual_prob, maxListSize, check_matrix,
                                  check_value, actualInformation)
+
+    def _check_domain(self, xyvd):
+        """The kernels run one domain end to end; the reference lets the vector distribution's
+        use_log drive the transforms and the decoder's the path metrics, so a mixed pair would
+        combine log rows with linear metrics (or the reverse) there: refused here."""
+        if bool(getattr(xyvd, "use_log", False)) != bool(self.use_log):
+            raise NotImplementedError("list decoding needs the decoder and the vector distribution in the same "
+                                      "domain (use_log=%s vs %s)" % (self.use_log, getattr(xyvd, "use_log", False)))
 
     def mergeInfoAndFrozen(self, actualInformation, frozenValues):
         merged = np.empty(self.length, dtype=np.int64)
@@ -448,8 +459,6 @@ def irSimulation(q, length, simulateChannel, make_xyVectorDistribution, numberOf
     if ir_version != 1:
         raise TypeError("ir2 (ir_version=2) fails in the reference itself (listDecode argument mismatch)")
     encDec = QaryPolarEncoderDecoder(q, length, frozenSet, commonRandomnessSeed, use_log=use_log)
-    if use_log:
-        raise NotImplementedError("list decoding runs in the linear domain only (use_log=False)")
     informationRNG = random.Random(randomInformationSeed)
     badKeys = badSymbols = 0
     probResultList = []
@@ -461,6 +470,7 @@ def irSimulation(q, length, simulateChannel, make_xyVectorDistribution, numberOf
             a = informationRNG.choices(range(0, q), k=encDec.length)
             b = simulateChannel(a)
             a_key, fv, _, _, xyvd = encDec._ir_inputs(a, b, make_xyVectorDistribution, checkSize)
+            encDec._check_domain(xyvd)
             keys.append(a_key)
             fvs.append(fv)
             xys.append(np.asarray(xyvd.probs, dtype=np.float64))

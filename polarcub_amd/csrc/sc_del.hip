@@ -22,13 +22,16 @@ constexpr int kMaxOnes = 3;
 DelKern del_kernel(int n0, int tb, bool exp, int ones) {
     if (ones < 0 || ones > kMaxOnes) return nullptr;
     const int oc = ones > 0 ? kMaxOnes : 0;
+#define PCUB_DEL_PICK(k) \
+    case k: return exp ? del_kernel_n##k##_x(tb, oc) : oc == 0 ? del_kernel_n##k##_d0(tb) : del_kernel_n##k##_d3(tb);
     switch (n0) {
-        case 1: return del_kernel_n1(tb, exp, oc);
-        case 2: return del_kernel_n2(tb, exp, oc);
-        case 3: return del_kernel_n3(tb, exp, oc);
-        case 4: return del_kernel_n4(tb, exp, oc);
+        PCUB_DEL_PICK(1)
+        PCUB_DEL_PICK(2)
+        PCUB_DEL_PICK(3)
+        PCUB_DEL_PICK(4)
         default: return nullptr;
     }
+#undef PCUB_DEL_PICK
 }
 
 // comb(ones, i) * (1 - pd)^i * pd^(ones - i), left to right as the reference evaluates it

@@ -157,6 +157,9 @@ struct DelCtx {
     double* xv;               // [256] collapsed values, codeword g's at [g*T, (g+1)*T)
     unsigned long long* xb;   // [LV] ballots of the encoding bits, one per local index
     unsigned long long* xub;  // [CPB][NW] decisions per codeword
+    // T > 64, export mode: per-codeword SC levels and encodings in LDS (see export_wide())
+    double* xe;               // [CPB][2T] node values, depth d at 2T - 2(T >> d)
+    uint8_t* xeb;             // [CPB][2T] left-child encodings (depth d at T - 2(T >> d)), then the current one
 
     // bits [k*T + 64w, ...) of a bit vector whose word i is w[i * stride]
     PCUB_HD uint64_t window(const uint32_t* w, int wi, long long stride = 1) const {
@@ -183,8 +186,9 @@ struct DelCtx {
         bool rate0 = true;
 #pragma unroll
         for (int w = 0; w < NW; ++w) rate0 = rate0 && (fm[w] == WM);
-        if constexpr (EXP) {
-            static_assert(T <= 64, "export mode: at most 64 trellises");
+        if constexpr (EXP && T > 64) {
+            y = export_wide(v, ub, fm, fv);
+        } else if constexpr (EXP) {
             y = XSubE<T, 0>::run(v, ub[0], fm[0], fv[0], lane, A.leaf + (long long)k * T * A.B + cw, A.B, leader) & 1u;
         } else if (rate0) {  // rate-0 node: decisions are the frozen values
 #pragma unroll
@@ -251,6 +255,75 @@ struct DelCtx {
             }
         }
         ++k;
+        return y;
+    }
+
+    // Export mode over T > 64 collapsed rows (the codeword's lanes span T/64 waves): SC over the
+    // node in LDS, level by level across the codeword's lanes with a workgroup barrier per level
+    // (every codeword of the group runs the same schedule), no node skipped, every leaf written
+    // at leaf[u * B] by the leader (BinaryPolarEncoderDecoder.py:268-273).  Values keep the
+    // half-split order of XSub: a node of length M at positions [0, M) has children
+    // op(v[p], v[p + M/2]) at [0, M/2), and its encoding is [ym ^ yp | yp].  The genie path,
+    // not the throughput path: ~3 barriers per leaf.
+    __device__ __forceinline__ uint32_t export_wide(double v, uint64_t* ub, const uint64_t* fm, const uint64_t* fv) {
+        constexpr int m = T == 128 ? 7 : 8;
+        static_assert(T == 128 || T == 256, "wide export: 128 or 256 trellises");
+        const int p = threadIdx.x & (T - 1);
+        const int g = threadIdx.x / T;
+        double* V = xe + g * 2 * T;
+        uint8_t* E = xeb + g * 2 * T;
+        uint8_t* C = E + T;
+        auto voff = [](int d) { return 2 * T - 2 * (T >> d); };
+        auto eoff = [](int d) { return T - 2 * (T >> d); };
+        V[p] = v;
+        __syncthreads();
+#pragma unroll 1
+        for (int i = 0; i < T; ++i) {
+            const int ds = i == 0 ? 0 : m - 1 - __builtin_ctz((unsigned)i);
+#pragma unroll 1
+            for (int d = ds; d < m; ++d) {
+                const int H = (T >> d) >> 1;
+                if (p < H) {
+                    const double a = V[voff(d) + p], b = V[voff(d) + p + H];
+                    V[voff(d + 1) + p] = (d == ds && i != 0) ? op_g(a, b, E[eoff(d + 1) + p]) : op_f(a, b);
+                }
+                __syncthreads();
+            }
+            const double c = V[voff(m)];
+            const int wi = i >> 6, bt = i & 63;
+            uint64_t fmw = fm[0], fvw = fv[0];
+#pragma unroll
+            for (int w = 1; w < NW; ++w)
+                if (wi == w) {
+                    fmw = fm[w];
+                    fvw = fv[w];
+                }
+            const uint32_t u = ((fmw >> bt) & 1ull) ? (uint32_t)((fvw >> bt) & 1ull) : leaf_v(c);
+            if (leader) A.leaf[((long long)k * T + i) * A.B + cw] = c;
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+                if (wi == w) ub[w] |= (uint64_t)u << bt;
+            __syncthreads();  // every lane has read the leaf before C / V are rewritten
+            if (p == 0) C[0] = (uint8_t)u;
+            __syncthreads();
+            int d = m;
+#pragma unroll 1
+            for (; d > 0 && ((i >> (m - d)) & 1); --d) {  // right child finished: combine into the parent
+                const int M = T >> d;
+                if (p < M) {
+                    const uint8_t e = C[p];
+                    C[p] = E[eoff(d) + p] ^ e;
+                    C[p + M] = e;
+                }
+                __syncthreads();
+            }
+            if (d > 0) {  // a left child finished: keep its encoding for its sibling's plus transform
+                if (p < (T >> d)) E[eoff(d) + p] = C[p];
+                __syncthreads();
+            }
+        }
+        const uint32_t y = C[p];
+        __syncthreads();  // C is rewritten by the next node's first leaf
         return y;
     }
 
@@ -432,12 +505,16 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
     __shared__ double xv[(T >= 64 && !EXP) ? kDelBlock : 1];
     __shared__ unsigned long long xb[(T >= 64 && !EXP) ? DelCtx<T, EXP>::LV : 1],
         xub[(T >= 64 && !EXP) ? CPB * DelCtx<T, EXP>::NW : 1];
+    __shared__ double xe[(T > 64 && EXP) ? 2 * kDelBlock : 1];
+    __shared__ uint8_t xeb[(T > 64 && EXP) ? 2 * kDelBlock : 1];
     DelCtx<T, EXP> cx;
+    cx.xe = xe;
+    cx.xeb = xeb;
     cx.xv = xv;
     cx.xb = xb;
     cx.xub = xub;
     cx.A = A;
-    cx.cw = cw;
+    cx.cw = c;  // clamped: padding groups read fval_cw in bounds; stores are leader-only
     cx.leader = valid && p == 0;
     cx.lane = lane;
     cx.k = 0;
@@ -476,54 +553,35 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
 
 typedef void (*DelKern)(DelArgs);
 
-// the kernel for (n0, n - n0) trellis shape, export mode, guard-band-ones capacity; or nullptr
-DelKern del_kernel_n1(int tb, bool exp, int oc);
-DelKern del_kernel_n2(int tb, bool exp, int oc);
-DelKern del_kernel_n3(int tb, bool exp, int oc);
-DelKern del_kernel_n4(int tb, bool exp, int oc);
+// the kernel for (n0, n - n0) trellis shape, export mode, guard-band-ones capacity (0 or 3); or
+// nullptr.  Defined in sc_del_n<n0>.hip (decode, OC 0), sc_del_n<n0>o.hip (decode, OC 3) and
+// sc_del_n<n0>x.hip (export).
+#define PCUB_DEL_TABLE(n0)                     \
+    DelKern del_kernel_n##n0##_d0(int tb);     \
+    DelKern del_kernel_n##n0##_d3(int tb);     \
+    DelKern del_kernel_n##n0##_x(int tb, int oc);
+PCUB_DEL_TABLE(1)
+PCUB_DEL_TABLE(2)
+PCUB_DEL_TABLE(3)
+PCUB_DEL_TABLE(4)
+#undef PCUB_DEL_TABLE
 
-// decode mode: T up to 256 (one workgroup), OC 0 or 3; export mode: T <= 64, OC 0
-template <int N0>
-DelKern del_kernel_tb(int tb, bool exp, int oc) {
-    if (exp) {
-        if (oc != 0) return nullptr;
-        switch (tb) {
-            case 1: return k_sc_del<N0, 1, true, 0>;
-            case 2: return k_sc_del<N0, 2, true, 0>;
-            case 3: return k_sc_del<N0, 3, true, 0>;
-            case 4: return k_sc_del<N0, 4, true, 0>;
-            case 5: return k_sc_del<N0, 5, true, 0>;
-            case 6: return k_sc_del<N0, 6, true, 0>;
-            default: return nullptr;
-        }
+// Kernel tables, one per translation-unit group (decode without / with guard-band ones, export),
+// so the large n0 = 3, 4 instantiations compile in parallel.  T up to 256 (one workgroup) in
+// every mode; OC 0 or 3.
+template <int N0, bool EXP, int OC>
+DelKern del_kernel_t(int tb) {
+    switch (tb) {
+        case 1: return k_sc_del<N0, 1, EXP, OC>;
+        case 2: return k_sc_del<N0, 2, EXP, OC>;
+        case 3: return k_sc_del<N0, 3, EXP, OC>;
+        case 4: return k_sc_del<N0, 4, EXP, OC>;
+        case 5: return k_sc_del<N0, 5, EXP, OC>;
+        case 6: return k_sc_del<N0, 6, EXP, OC>;
+        case 7: return k_sc_del<N0, 7, EXP, OC>;
+        case 8: return k_sc_del<N0, 8, EXP, OC>;
+        default: return nullptr;
     }
-    if (oc == 0) {
-        switch (tb) {
-            case 1: return k_sc_del<N0, 1, false, 0>;
-            case 2: return k_sc_del<N0, 2, false, 0>;
-            case 3: return k_sc_del<N0, 3, false, 0>;
-            case 4: return k_sc_del<N0, 4, false, 0>;
-            case 5: return k_sc_del<N0, 5, false, 0>;
-            case 6: return k_sc_del<N0, 6, false, 0>;
-            case 7: return k_sc_del<N0, 7, false, 0>;
-            case 8: return k_sc_del<N0, 8, false, 0>;
-            default: return nullptr;
-        }
-    }
-    if (oc == 3) {
-        switch (tb) {
-            case 1: return k_sc_del<N0, 1, false, 3>;
-            case 2: return k_sc_del<N0, 2, false, 3>;
-            case 3: return k_sc_del<N0, 3, false, 3>;
-            case 4: return k_sc_del<N0, 4, false, 3>;
-            case 5: return k_sc_del<N0, 5, false, 3>;
-            case 6: return k_sc_del<N0, 6, false, 3>;
-            case 7: return k_sc_del<N0, 7, false, 3>;
-            case 8: return k_sc_del<N0, 8, false, 3>;
-            default: return nullptr;
-        }
-    }
-    return nullptr;
 }
 
 }  // namespace pcub

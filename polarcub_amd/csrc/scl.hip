@@ -56,10 +56,12 @@ extern "C" size_t pcub_scl_qary_workspace(int64_t B, int32_t q, int32_t log2N, i
     return (size_t)scl_grid(B) * kSclBlock * scl_slot_bytes(q, log2N, L, K) + 16;
 }
 
-extern "C" int pcub_scl_qary(const double* xy, int64_t B, int32_t q, int32_t log2N, int32_t L,
-                             const uint8_t* frozen, const uint8_t* frozen_vals, int32_t nF, const uint8_t* actual,
-                             int32_t K, uint8_t* out_info, double* out_prob, int32_t* out_size, double* out_actual,
-                             void* workspace, size_t workspace_bytes, void* stream) {
+namespace {
+
+int launch_scl(bool lg, const double* xy, int64_t B, int32_t q, int32_t log2N, int32_t L, const uint8_t* frozen,
+               const uint8_t* frozen_vals, int32_t nF, const uint8_t* actual, int32_t K, uint8_t* out_info,
+               double* out_prob, int32_t* out_size, double* out_actual, void* workspace, size_t workspace_bytes,
+               void* stream) {
     if (!scl_args_ok(B, q, log2N, L, K) || !frozen || nF < 0 || nF + K != (1 << log2N)) return PCUB_EINVAL;
     if (B == 0) return 0;
     if (!xy || (nF > 0 && !frozen_vals) || !out_info || !out_prob || !out_size || !workspace) return PCUB_EINVAL;
@@ -86,9 +88,29 @@ extern "C" int pcub_scl_qary(const double* xy, int64_t B, int32_t q, int32_t log
     A.out_prob = out_prob;
     A.out_size = (int*)out_size;
     A.out_actual = out_actual;
+    A.log = lg ? 1 : 0;
     A.ns = g * kSclBlock;
     A.cells = (double*)workspace;
     A.bytes = (uint8_t*)workspace + (size_t)Y.ncells * 8 * (size_t)A.ns;
     hipLaunchKernelGGL(k_scl, dim3((unsigned)g), dim3(kSclBlock), 0, (hipStream_t)stream, A);
     return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int pcub_scl_qary(const double* xy, int64_t B, int32_t q, int32_t log2N, int32_t L,
+                             const uint8_t* frozen, const uint8_t* frozen_vals, int32_t nF, const uint8_t* actual,
+                             int32_t K, uint8_t* out_info, double* out_prob, int32_t* out_size, double* out_actual,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+    return launch_scl(false, xy, B, q, log2N, L, frozen, frozen_vals, nF, actual, K, out_info, out_prob, out_size,
+                      out_actual, workspace, workspace_bytes, stream);
+}
+
+// use_log=True: xy holds log-probabilities; out_prob / out_actual are log-domain metrics
+extern "C" int pcub_scl_qary_log(const double* xy, int64_t B, int32_t q, int32_t log2N, int32_t L,
+                                 const uint8_t* frozen, const uint8_t* frozen_vals, int32_t nF, const uint8_t* actual,
+                                 int32_t K, uint8_t* out_info, double* out_prob, int32_t* out_size, double* out_actual,
+                                 void* workspace, size_t workspace_bytes, void* stream) {
+    return launch_scl(true, xy, B, q, log2N, L, frozen, frozen_vals, nF, actual, K, out_info, out_prob, out_size,
+                      out_actual, workspace, workspace_bytes, stream);
 }

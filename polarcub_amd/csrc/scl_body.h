@@ -32,11 +32,20 @@
 // reference's [-k:] slice of order statistics).  Without ties the surviving path SET and its
 // metrics are the reference's.
 //
+// Log domain (use_log=True, SclArgs::log): rows are log-probabilities; the transforms use numpy's
+// logaddexp and scipy's logsumexp normalisation (as sc_qary_log.hip), path metrics add, a prune
+// keeps min(count of non -inf, L), normalize subtracts the largest, reliability is (second largest
+// - largest), and each product becomes the sum the reference forms: np.sum over a node's positions
+// (numpy's pairwise summation, np_sum_pow2), Python's sum over the row maxima and np.sum(axis=1)
+// over a fork's selected entries (both left to right).  exp / log1p / log are the platform's, so
+// log-domain values agree with the reference to a few ulps (the tests state the tolerance).
+//
 // One lane per codeword; all per-codeword state in a slab of 8-byte cells and a slab of bytes,
 // element e at [e * ns] (slot-minor: a wave's lanes touch consecutive words).  The recursion's
 // shape depends only on the frozen mask.  The actual information's path (listDecode's
 // actualInformation) is tracked in path slot L: its distributions, encodings and actual_prob.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #include "sc_common.h"
@@ -55,6 +64,7 @@ struct SclArgs {
     double* out_prob;        // [L][B] final normalised path metrics
     int* out_size;           // [B] final list size
     double* out_actual;      // [B] actual_prob (when actual is given)
+    int log;                 // 1: log-domain rows and metrics (use_log=True)
     double* cells;           // slab of 8-byte cells  [ncells][ns]
     uint8_t* bytes;          // slab of bytes         [nbytes][ns]
     long long ns;
@@ -107,6 +117,7 @@ struct SclCtx {
     int fi;          // next frozen value
     int buf;         // current information buffer
     bool track;      // actual path present
+    bool lg;         // log domain
     double actual_prob;
 
     PCUB_HD double& C(long long e) { return cells[e * ns]; }
@@ -120,9 +131,51 @@ struct SclCtx {
     PCUB_HD int actual_sym(int ii) { return (int)A->actual[(long long)ii * A->B + cw]; }
 };
 
+constexpr double kSclLn2 = 0.693147180559945309417232121458176568;
+
+// numpy's npy_logaddexp
+PCUB_HD double scl_logaddexp(double x, double y) {
+    if (x == y) return x + kSclLn2;
+    const double t = x - y;
+    if (t > 0) return x + log1p(exp(-t));
+    if (t <= 0) return y + log1p(exp(t));
+    return t;  // NaN
+}
+
+// scipy 1.15's logsumexp of q <= 8 values (every maximal element taken out of the sum), as
+// sc_qary_log.hip
+PCUB_HD double scl_logsumexp(const double* p, int q) {
+    double mx = p[0];
+    for (int x = 1; x < q; ++x) mx = p[x] > mx ? p[x] : mx;
+    double m = 0.0;
+    for (int x = 0; x < q; ++x) m += (p[x] == mx) ? 1.0 : 0.0;
+    const double shift = isfinite(mx) ? mx : 0.0;
+    double rest = 0.0;
+    for (int x = 1; x < q; ++x) rest += (p[x] == mx) ? 0.0 : exp(p[x] - shift);
+    double s = ((p[0] == mx) ? 0.0 : exp(p[0] - shift)) + rest;
+    if (s != 0.0) s = s / m;
+    return log1p(s) + log(m) + mx;
+}
+
+// metric (x) factor: product, or sum in the log domain
+PCUB_HD double scl_mul(const SclCtx& c, double p, double f) { return c.lg ? p + f : p * f; }
+
+// actual_prob update by a factor v and a normalisation weight w (:467-470)
+PCUB_HD void scl_scale_actual(SclCtx& c, double v, double w) {
+    if (c.lg) c.actual_prob += v - w;
+    else c.actual_prob *= v / w;
+}
+
 // leaf marginal of a length-1 row into C(c_row + off .. + q)
 PCUB_HD void scl_marginal(SclCtx& c, int d, int slot, long long off) {
     const int q = c.Y.q;
+    if (c.lg) {
+        double r[8];
+        for (int x = 0; x < q; ++x) r[x] = c.row(d, slot, 0, x);
+        const double s = scl_logsumexp(r, q);
+        for (int x = 0; x < q; ++x) c.C(off + x) = s > -INFINITY ? r[x] - s : -log((double)q);
+        return;
+    }
     double s = 0.0;
     for (int x = 0; x < q; ++x) s = s + c.row(d, slot, 0, x);
     for (int x = 0; x < q; ++x) c.C(off + x) = s > 0.0 ? c.row(d, slot, 0, x) / s : 1.0 / q;
@@ -154,8 +207,9 @@ PCUB_HD int scl_prune(SclCtx& c, int ncand) {
         for (int i = 0; i < ncand; ++i) c.C(c.Y.c_flag + i) = 1.0;
         return ncand;
     }
-    int nz = 0;
-    for (int i = 0; i < ncand; ++i) nz += c.C(c.Y.c_cand + i) != 0.0;
+    int nz = 0;  // count_nonzero, or the count of entries that are not -inf (log domain)
+    const double zero = c.lg ? -INFINITY : 0.0;
+    for (int i = 0; i < ncand; ++i) nz += c.C(c.Y.c_cand + i) != zero;
     // (all candidates zero: the reference fails on the empty list; keep the first one)
     const int keep = nz < L ? (nz > 0 ? nz : 1) : L;
     for (int r = 0; r < keep; ++r) {
@@ -178,7 +232,7 @@ PCUB_HD int scl_prune(SclCtx& c, int ncand) {
 PCUB_HD double scl_normalize(SclCtx& c, int k) {
     double mx = c.C(c.Y.c_prob);
     for (int i = 1; i < k; ++i) mx = c.C(c.Y.c_prob + i) > mx ? c.C(c.Y.c_prob + i) : mx;
-    for (int i = 0; i < k; ++i) c.C(c.Y.c_prob + i) = c.C(c.Y.c_prob + i) / mx;
+    for (int i = 0; i < k; ++i) c.C(c.Y.c_prob + i) = c.lg ? c.C(c.Y.c_prob + i) - mx : c.C(c.Y.c_prob + i) / mx;
     return mx;
 }
 
@@ -196,7 +250,7 @@ PCUB_HD double scl_ratio(SclCtx& c, int d, int slot, int pos) {
             lo = v;
         }
     }
-    return lo / hi;
+    return c.lg ? lo - hi : lo / hi;
 }
 
 PCUB_HD int scl_argmax(SclCtx& c, int d, int slot, int pos, double* mx) {
@@ -256,8 +310,46 @@ PCUB_HD int scl_commit(SclCtx& c, int ncand, int ii, int div, int lin, int* orig
     return k;
 }
 
+// numpy's pairwise sum (the add reduction's inner loop) of positions [off, off + n), n <= 128,
+// of row_j[enc_j]
+PCUB_HD double scl_np_block(SclCtx& c, int d, int slot, long long e, int off, int n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int i = 0; i < n; ++i) r += c.row(d, slot, off + i, c.Bt(e + off + i));
+        return r;
+    }
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = c.row(d, slot, off + j, c.Bt(e + off + j));
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; ++j) r[j] += c.row(d, slot, off + i + j, c.Bt(e + off + i + j));
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += c.row(d, slot, off + i, c.Bt(e + off + i));
+    return res;
+}
+
+// np.sum of row_j[enc_j] over the S (a power of two) positions of a node: numpy halves blocks
+// longer than 128 (n2 = n/2 - (n/2) % 8 = n/2 here) and sums the halves, so the 128-blocks combine
+// in a balanced binary tree, left + right (a carry chain over the block index)
+PCUB_HD double scl_np_sum_pow2(SclCtx& c, int d, int slot, int S, long long e) {
+    if (S <= 128) return scl_np_block(c, d, slot, e, 0, S);
+    double acc[6];
+    const int nb = S / 128;
+    for (int b = 0; b < nb; ++b) {
+        double v = scl_np_block(c, d, slot, e, b * 128, 128);
+        int lvl = 0;
+        for (; (b >> lvl) & 1; ++lvl) v = acc[lvl] + v;
+        acc[lvl] = v;
+    }
+    int top = 0;
+    while ((1 << top) < nb) ++top;
+    return acc[top];
+}
+
 // product over the S positions of a node of row_j[enc_j] (enc bytes at e), left to right
+// (np.product); the log domain's np.sum
 PCUB_HD double scl_prod_enc(SclCtx& c, int d, int slot, int S, long long e) {
+    if (c.lg) return scl_np_sum_pow2(c, d, slot, S, e);
     double p = c.row(d, slot, 0, c.Bt(e));
     for (int j = 1; j < S; ++j) p = p * c.row(d, slot, j, c.Bt(e + j));
     return p;
@@ -283,7 +375,8 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
             if (nin == 1) {  // information leaf: q forks per path
                 for (int i = 0; i < Lin; ++i) {
                     scl_marginal(c, d, i, Y.c_row);
-                    for (int s = 0; s < q; ++s) c.C(Y.c_cand + s * Lin + i) = c.C(Y.c_prob + i) * c.C(Y.c_row + s);
+                    for (int s = 0; s < q; ++s)
+                        c.C(Y.c_cand + s * Lin + i) = scl_mul(c, c.C(Y.c_prob + i), c.C(Y.c_row + s));
                 }
                 const int nc = Lin * q;
                 scl_prune(c, nc);
@@ -298,7 +391,7 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
                 if (c.track) {
                     const int a = c.actual_sym(ii);
                     scl_marginal(c, d, L, Y.c_row);
-                    c.actual_prob *= c.C(Y.c_row + a) / w;
+                    scl_scale_actual(c, c.C(Y.c_row + a), w);
                     c.Bt(Y.enc(d, side, L, 0)) = (uint8_t)a;
                 }
                 return k;
@@ -306,14 +399,14 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
             const int fv = c.frozen_value();  // frozen leaf
             for (int i = 0; i < Lin; ++i) {
                 scl_marginal(c, d, i, Y.c_row);
-                c.C(Y.c_prob + i) = c.C(Y.c_prob + i) * c.C(Y.c_row + fv);
+                c.C(Y.c_prob + i) = scl_mul(c, c.C(Y.c_prob + i), c.C(Y.c_row + fv));
                 c.Bt(Y.enc(d, side, i, 0)) = (uint8_t)fv;
                 c.C(mapo + i) = (double)i;
             }
             const double w = scl_normalize(c, Lin);
             if (c.track) {
                 scl_marginal(c, d, L, Y.c_row);
-                c.actual_prob *= c.C(Y.c_row + fv) / w;
+                scl_scale_actual(c, c.C(Y.c_row + fv), w);
                 c.Bt(Y.enc(d, side, L, 0)) = (uint8_t)fv;
             }
             return Lin;
@@ -326,13 +419,13 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
             for (int j = 0; j < S; ++j) c.Bt(tv + j) = (uint8_t)c.frozen_value();
             scl_polar(c, tv, to, tt, S);
             for (int i = 0; i < Lin; ++i) {
-                c.C(Y.c_prob + i) = c.C(Y.c_prob + i) * scl_prod_enc(c, d, i, S, to);
+                c.C(Y.c_prob + i) = scl_mul(c, c.C(Y.c_prob + i), scl_prod_enc(c, d, i, S, to));
                 for (int j = 0; j < S; ++j) c.Bt(Y.enc(d, side, i, j)) = c.Bt(to + j);
                 c.C(mapo + i) = (double)i;
             }
             const double w = scl_normalize(c, Lin);
             if (c.track) {
-                c.actual_prob *= scl_prod_enc(c, d, L, S, to) / w;
+                scl_scale_actual(c, scl_prod_enc(c, d, L, S, to), w);
                 for (int j = 0; j < S; ++j) c.Bt(Y.enc(d, side, L, j)) = c.Bt(to + j);
             }
             return Lin;
@@ -350,7 +443,7 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
             for (int i = 0; i < Lin; ++i)
                 for (int s = 0; s < q; ++s)
                     c.C(Y.c_cand + s * Lin + i) =
-                        c.C(Y.c_prob + i) * scl_prod_enc(c, d, i, S, Y.b_tmp + (long long)s * Y.N);
+                        scl_mul(c, c.C(Y.c_prob + i), scl_prod_enc(c, d, i, S, Y.b_tmp + (long long)s * Y.N));
             const int nc = Lin * q;
             scl_prune(c, nc);
             const int k = scl_commit(c, nc, ii, 0, Lin, origin);
@@ -363,7 +456,7 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
             const double w = scl_normalize(c, k);
             if (c.track) {
                 const int a = c.actual_sym(ii);
-                c.actual_prob *= scl_prod_enc(c, d, L, S, Y.b_tmp + (long long)a * Y.N) / w;
+                scl_scale_actual(c, scl_prod_enc(c, d, L, S, Y.b_tmp + (long long)a * Y.N), w);
                 for (int j = 0; j < S; ++j) c.Bt(Y.enc(d, side, L, j)) = c.Bt(Y.b_tmp + (long long)a * Y.N + j);
             }
             return k;
@@ -388,10 +481,10 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
                     if (sel) continue;
                     double mx;
                     csum += scl_argmax(c, d, i, j, &mx);
-                    pm = first ? mx : pm * mx;
+                    pm = first ? mx : (c.lg ? pm + mx : pm * mx);  // Python's sum from 0 / np.product
                     first = false;
                 }
-                base = first ? base * 1.0 : base * pm;
+                base = c.lg ? base + (first ? 0.0 : pm) : (first ? base * 1.0 : base * pm);
                 const int delta = ((fv - csum) % q + q) % q;
                 for (int f = 0; f < fork; ++f) {
                     int sym[4];
@@ -403,8 +496,8 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
                     }
                     if (spc) sym[3] = ((delta - ssum) % q + q) % q;
                     double p = c.row(d, i, idx[0], sym[0]);
-                    for (int t = 1; t < nsel; ++t) p = p * c.row(d, i, idx[t], sym[t]);
-                    c.C(Y.c_cand + (long long)fork * i + f) = p * base;
+                    for (int t = 1; t < nsel; ++t) p = scl_mul(c, p, c.row(d, i, idx[t], sym[t]));
+                    c.C(Y.c_cand + (long long)fork * i + f) = c.lg ? p + base : p * base;
                 }
             }
             const int nc = Lin * fork;
@@ -447,7 +540,7 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
                     c.Bt(tv + j) = (uint8_t)(src < 0 ? fv : c.actual_sym(ii + src));
                 }
                 scl_polar(c, tv, to, tt, S);
-                c.actual_prob *= scl_prod_enc(c, d, L, S, to) / w;
+                scl_scale_actual(c, scl_prod_enc(c, d, L, S, to), w);
                 for (int j = 0; j < S; ++j) c.Bt(Y.enc(d, side, L, j)) = c.Bt(to + j);
             }
             return k;
@@ -458,6 +551,13 @@ PCUB_HD int scl_special(SclCtx& c, int d, int u0, int ii, int side, int Lin, int
 
 PCUB_HD bool scl_is_special(int S, int nin) { return S == 1 || nin <= 1 || nin >= S - 1; }
 
+// log-domain normalise (t = logsumexp; if t != -inf: p - t) and store a row at depth d
+PCUB_HD void scl_store_log(SclCtx& c, int d, int slot, int h, const double* o) {
+    const int q = c.Y.q;
+    const double t = scl_logsumexp(o, q);
+    for (int u = 0; u < q; ++u) c.C(c.Y.dist(d, slot, h, u)) = t != -INFINITY ? o[u] - t : o[u];
+}
+
 // General node, before its minus child (:684-700): the minus transform + sum-normalise of every
 // path's vector (and the actual path's) into depth d + 1.
 PCUB_HD void scl_minus(SclCtx& c, int d, int slot_in, int slot_out) {
@@ -465,6 +565,16 @@ PCUB_HD void scl_minus(SclCtx& c, int d, int slot_in, int slot_out) {
     const int q = Y.q, H = (Y.N >> d) / 2;
     for (int h = 0; h < H; ++h) {
         double o[8];
+        if (c.lg) {
+            for (int u = 0; u < q; ++u) o[u] = -INFINITY;
+            for (int x1 = 0; x1 < q; ++x1)
+                for (int x2 = 0; x2 < q; ++x2) {
+                    const int u = (x1 + x2) % q;
+                    o[u] = scl_logaddexp(o[u], c.row(d, slot_in, 2 * h, x1) + c.row(d, slot_in, 2 * h + 1, x2));
+                }
+            scl_store_log(c, d + 1, slot_out, h, o);
+            continue;
+        }
         for (int u = 0; u < q; ++u) o[u] = 0.0;
         for (int x1 = 0; x1 < q; ++x1)
             for (int x2 = 0; x2 < q; ++x2) {
@@ -485,6 +595,13 @@ PCUB_HD void scl_plus(SclCtx& c, int d, int slot_in, int slot_out, long long enc
     for (int h = 0; h < H; ++h) {
         const int u1 = c.Bt(encm + h);
         double o[8];
+        if (c.lg) {
+            for (int u2 = 0; u2 < q; ++u2)
+                o[u2] = scl_logaddexp(-INFINITY, c.row(d, slot_in, 2 * h, (u1 + u2) % q) +
+                                                     c.row(d, slot_in, 2 * h + 1, (q - u2) % q));
+            scl_store_log(c, d + 1, slot_out, h, o);
+            continue;
+        }
         for (int u2 = 0; u2 < q; ++u2)
             o[u2] = 0.0 + c.row(d, slot_in, 2 * h, (u1 + u2) % q) * c.row(d, slot_in, 2 * h + 1, (q - u2) % q);
         double t = 0.0;
@@ -582,8 +699,9 @@ PCUB_HD void scl_decode_cw(const SclArgs& A, long long cw, long long slot, bool 
     c.fi = 0;
     c.buf = 0;
     c.track = A.actual != nullptr;
-    c.actual_prob = 1.0;
-    c.C(c.Y.c_prob) = 1.0;
+    c.lg = A.log != 0;
+    c.actual_prob = c.lg ? 0.0 : 1.0;
+    c.C(c.Y.c_prob) = c.lg ? 0.0 : 1.0;
     const int k = scl_run(c);
     if (!store) return;
     const long long B = A.B;

@@ -484,8 +484,9 @@ class QaryListDecoder:
     """Batched q-ary SCL / Fast-SSC list decoding (pcub_scl_qary): QaryPolarEncoderDecoder.listDecode
     for B codewords of one code at list size L, with optional actual information words."""
 
-    def __init__(self, q, N, frozen_mask, L, device=None):
+    def __init__(self, q, N, frozen_mask, L, device=None, use_log=False):
         self.q, self.N, self.L = int(q), int(N), int(L)
+        self.use_log = bool(use_log)  # log-probability rows and metrics (pcub_scl_qary_log)
         self.n = _log2(self.N)
         if not 2 <= self.q <= 8 or not 1 <= self.L <= 64 or self.n > 12:
             raise ValueError("list decoder needs 2 <= q <= 8, 1 <= L <= 64, N <= 4096")
@@ -498,9 +499,11 @@ class QaryListDecoder:
         self.frozen_dev = torch.from_numpy(mask.copy()).to(self.device)
         self._ws = None
 
-    def decode_native(self, xy, frozen_vals, actual=None):
+    def decode_native(self, xy, frozen_vals, actual=None, max_workspace_bytes=None):
         """xy [N, B, q] f64, frozen_vals [nF, B] u8, actual [K, B] u8 or None (device tensors)
-        -> (info [L, K, B] u8, prob [L, B] f64, size [B] i32, actual_prob [B] f64 | None)."""
+        -> (info [L, K, B] u8, prob [L, B] f64, size [B] i32, actual_prob [B] f64 | None).
+        The slot slab is capped at max_workspace_bytes (default: half the free device memory);
+        fewer resident slots then stride over the batch."""
         if xy.dtype != torch.float64 or xy.dim() != 3 or xy.shape[0] != self.N or xy.shape[2] != self.q:
             raise ValueError("xy must be float64 [N, B, q] with N=%d, q=%d" % (self.N, self.q))
         xy = xy.contiguous()
@@ -510,16 +513,22 @@ class QaryListDecoder:
             torch.zeros((1, B), dtype=torch.uint8, device=dev)
         act = None if actual is None else actual.to(device=dev, dtype=torch.uint8).contiguous()
         need = int(_lib.lib().pcub_scl_qary_workspace(B, self.q, self.n, self.L, self.K))
+        # The full resident grid of slots can exceed device memory at large N*L*q: cap the slab at
+        # half of the free memory (at least one workgroup's slots); pcub_scl_qary then clips the grid.
+        block = int(_lib.lib().pcub_scl_qary_workspace(1, self.q, self.n, self.L, self.K))
+        free = torch.cuda.mem_get_info(dev)[0] + (0 if self._ws is None else self._ws.numel())
+        need = min(need, max(block, free // 2 if max_workspace_bytes is None else int(max_workspace_bytes)))
         if self._ws is None or self._ws.numel() < need:
+            self._ws = None
             self._ws = torch.empty(max(need, 16), dtype=torch.uint8, device=dev)
         info = torch.empty((self.L, max(1, self.K), B), dtype=torch.uint8, device=dev)
         prob = torch.empty((self.L, B), dtype=torch.float64, device=dev)
         size = torch.empty(B, dtype=torch.int32, device=dev)
         ap = torch.empty(B, dtype=torch.float64, device=dev) if act is not None else None
-        rc = _lib.lib().pcub_scl_qary(_p(xy), B, self.q, self.n, self.L, _p(self.frozen_dev), _p(fv), self.nF, _p(act),
-                                      self.K, _p(info), _p(prob), _p(size), _p(ap), _p(self._ws), self._ws.numel(),
-                                      _stream())
-        _lib.check(rc, "pcub_scl_qary")
+        fn = _lib.lib().pcub_scl_qary_log if self.use_log else _lib.lib().pcub_scl_qary
+        rc = fn(_p(xy), B, self.q, self.n, self.L, _p(self.frozen_dev), _p(fv), self.nF, _p(act), self.K, _p(info),
+                _p(prob), _p(size), _p(ap), _p(self._ws), self._ws.numel(), _stream())
+        _lib.check(rc, "pcub_scl_qary_log" if self.use_log else "pcub_scl_qary")
         return info[:, :self.K], prob, size, ap
 
     def decode(self, xy, frozen_vals, actual=None):
@@ -527,10 +536,11 @@ class QaryListDecoder:
         prob [B, L], size [B], actual_prob [B] | None)."""
         dev = self.device
         x = transpose_pairs(torch.as_tensor(np.ascontiguousarray(xy, np.float64), device=dev))
-        fv = torch.as_tensor(np.ascontiguousarray(np.asarray(frozen_vals, np.uint8).reshape(-1, self.nF).T),
+        B = x.shape[1]
+        fv = torch.as_tensor(np.ascontiguousarray(np.asarray(frozen_vals, np.uint8).reshape(B, self.nF).T),
                              device=dev)
         act = None if actual is None else torch.as_tensor(
-            np.ascontiguousarray(np.asarray(actual, np.uint8).reshape(-1, self.K).T), device=dev)
+            np.ascontiguousarray(np.asarray(actual, np.uint8).reshape(B, self.K).T), device=dev)
         info, prob, size, ap = self.decode_native(x, fv, act)
         return (info.permute(2, 0, 1).cpu().numpy(), prob.t().cpu().numpy(), size.cpu().numpy(),
                 None if ap is None else ap.cpu().numpy())

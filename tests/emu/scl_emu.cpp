@@ -9,7 +9,7 @@
 
 extern "C" int emu_scl(const double* xy, long long B, int q, int n, int L, const uint8_t* frozen,
                        const uint8_t* fvals, int nF, const uint8_t* actual, int K, uint8_t* out_info,
-                       double* out_prob, int* out_size, double* out_actual) {
+                       double* out_prob, int* out_size, double* out_actual, int use_log) {
     pcub::SclLayout Y;
     Y.init(n, q, L, K);
     std::vector<double> cells((size_t)Y.ncells);
@@ -29,6 +29,7 @@ extern "C" int emu_scl(const double* xy, long long B, int q, int n, int L, const
     A.out_prob = out_prob;
     A.out_size = out_size;
     A.out_actual = out_actual;
+    A.log = use_log;
     A.cells = cells.data();
     A.bytes = bytes.data();
     A.ns = 1;

@@ -110,3 +110,48 @@ def test_test2_cli_matches_reference_run():
     with contextlib.redirect_stdout(buf):
         test2.main(["--seed", str(g["meta"]["global_random_seed"])])
     assert buf.getvalue().strip().splitlines() == g["meta"]["lines"]
+
+
+@pytest.mark.parametrize("ci", range(6))
+def test_genie_deletion_wide_matches_reference(ci, monkeypatch):
+    """Genie runs past 64 trellises per codeword (main_deletion's own n0 = n//3 at n = 10: 128;
+    n0 = 1 at n = 8 / 9: 128 / 256) and with guard-band ones 1..3: every trial's leaves come from
+    the GPU export kernel (the host recursion is disabled here), TV + Pe and the frozen set equal
+    the reference run's."""
+    from polarcub_amd import coding, deletion, sc, vectors
+    g = load_golden("deletion_genie_wide")
+    xi = g["meta"]["xi"]
+    n, n0, ones, G = (int(v) for v in g["c%d_shape" % ci])
+    pd = float(g["c%d_pd" % ci][0])
+    N = 1 << n
+    assert sc.leaf_deletion_supported(n, n0, ones)
+    monkeypatch.setattr(coding.BinaryPolarEncoderDecoder, "genieSingleDecodeSimulatioan",
+                        lambda *a, **k: pytest.fail("host genie decode used"))
+    crng = random.Random()
+    crng.seed(100 + ci)
+
+    def make_x():
+        v = vectors.BinaryMemorylessVectorDistribution(N)
+        v.probs[:] = 0.5
+        return v
+
+    frozen, cap = _run_capturing(lambda: coding.genieEncodeDecodeSimulation(
+        N, make_x, lambda e: deletion.addDeletionGuardBands(e, n, n0, xi, ones),
+        lambda c: deletion.deletionChannelSimulation(c, pd, None, crng),
+        lambda r: deletion.buildCollectionOfBinaryTrellises_uniformInput_deletion(r, pd, xi, n, n0, ones),
+        G, 0.1, 300 + ci, trustXYProbs=n <= n0))
+    assert np.array_equal(cap["TV"] + cap["Pe"], g["c%d_score" % ci])
+    assert np.array_equal(np.array([1 if i in frozen else 0 for i in range(N)], np.uint8), g["c%d_frozen" % ci])
+
+
+def test_main_deletion_cli_n10_matches_reference_run():
+    """main_deletion -n 10 -g 6 -e 4 (n0 = 3: 128 trellises a codeword, genie and decode on the GPU)
+    prints the reference run's lines."""
+    from polarcub_amd.cli import main_deletion
+    g = load_golden("deletion_genie_wide")
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        main_deletion.main(list(g["meta"]["main_argv"]))
+    lines = [l for l in buf.getvalue().strip().splitlines()
+             if not l.startswith(("TVVec", "pevec", "HEncvec", "HDecvec"))]
+    assert lines == g["meta"]["main_lines"]

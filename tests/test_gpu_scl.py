@@ -111,3 +111,102 @@ def test_gpu_list_decoder_full_occupancy(sc):
     info1, prob1, size1, _ = dec.decode_native(xy[:, :6].contiguous(), fv[:, :6].contiguous())
     assert torch.equal(size[:6], size1)
     assert torch.equal(info[:, :, :6], info1) and torch.equal(prob[:, :6], prob1)
+
+
+def test_gpu_list_decoder_workspace_capped(sc):
+    """A slab smaller than the resident grid needs (here forced to 1/16 of it) clips the grid: the
+    launcher strides fewer slots over the batch and every codeword decodes as it does alone.  The
+    default cap (half the free memory) keeps the slab of a large shape (N=4096, q=4, L=32: about
+    4 MB a slot, hundreds of GB for the full grid) inside the device.  K = N (nothing frozen)
+    through decode()."""
+    import torch
+    from polarcub_amd import _lib
+    rng = np.random.default_rng(11)
+    q, n, L, B = 4, 8, 8, 1 << 16
+    N = 1 << n
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    dec = sc.QaryListDecoder(q, N, frozen, L)
+    K = N - int(frozen.sum())
+    full = int(_lib.lib().pcub_scl_qary_workspace(B, q, n, L, K))
+    xy = torch.rand((N, B, q), dtype=torch.float64, device="cuda")
+    fv = torch.zeros((int(frozen.sum()), B), dtype=torch.uint8, device="cuda")
+    info, prob, size, _ = dec.decode_native(xy, fv, max_workspace_bytes=full // 16)
+    torch.cuda.synchronize()
+    assert dec._ws.numel() <= full // 16 + 64
+    idx = [0, 1, B // 2, B - 1]
+    info1, prob1, size1, _ = sc.QaryListDecoder(q, N, frozen, L).decode_native(xy[:, idx].contiguous(),
+                                                                               fv[:, idx].contiguous())
+    assert torch.equal(size[idx], size1)
+    assert torch.equal(info[:, :, idx], info1) and torch.equal(prob[:, idx], prob1)
+    big = int(_lib.lib().pcub_scl_qary_workspace(1 << 17, 4, 12, 32, 2048))
+    assert big > torch.cuda.get_device_properties(0).total_memory  # why the cap exists
+    d0 = sc.QaryListDecoder(2, 16, np.zeros(16, np.uint8), 4)
+    i0, p0, s0, _ = d0.decode(rng.random((3, 16, 2)), np.zeros((3, 0), np.uint8))
+    assert i0.shape == (3, 4, 16) and (s0 >= 1).all()
+
+
+# -- log domain (pcub_scl_qary_log) -------------------------------------------------------------
+from tests.test_scl import _close_log, _log_inputs, _oracle_log_with_gap, ir_closures_log  # noqa: E402
+
+
+def test_gpu_log_list_decoder_matches_reference_sets(sc):
+    """use_log=True list decoding on the GPU against the reference's own log-domain runs
+    (tests/golden/scl_log.npz): path sets, metrics and actual_prob within the log tolerance."""
+    g = load_golden("scl_log")
+    for c in g["meta"]["cases"]:
+        t_, q, L = c["tag"], c["q"], c["L"]
+        info, prob, size, ap = sc.QaryListDecoder(q, 1 << c["n"], g[t_ + "_frozen"], L, use_log=True).decode(
+            g[t_ + "_xy"], g[t_ + "_fv"], g[t_ + "_actual"])
+        for t in range(g[t_ + "_xy"].shape[0]):
+            rk = int(g[t_ + "_size"][t])
+            assert size[t] == rk
+            ours = _as_set(info[t][:rk].tolist(), prob[t][:rk].tolist())
+            ref = _as_set(g[t_ + "_info"][t][:rk].tolist(), g[t_ + "_prob"][t][:rk].tolist())
+            assert [a for a, _ in ours] == [a for a, _ in ref]
+            assert _close_log([p for _, p in ours], [p for _, p in ref])
+            assert _close_log(ap[t], g[t_ + "_aprob"][t])
+
+
+@pytest.mark.parametrize("q,n,L", [(2, 4, 4), (3, 5, 4), (4, 6, 8), (4, 8, 4), (2, 9, 2)])
+def test_gpu_log_list_decoder_matches_oracle(sc, monkeypatch, q, n, L):
+    rng = np.random.default_rng(700 * q + 10 * n + L)
+    frozen, xy, fv, act = _log_inputs(rng, q, n, 8, False)
+    if n >= 8:  # a long rate-0 half, then a rate-1 (n = 8) / repetition (n = 9) half, peaked rows
+        N = 1 << n
+        frozen[: N // 2] = 1
+        frozen[N // 2:] = 0 if n == 8 else 1
+        frozen[N - 1] = 0
+        K = int((frozen == 0).sum())
+        fv = rng.integers(0, q, (8, N - K))
+        act = rng.integers(0, q, (8, K))
+        y = rng.integers(0, q, (8, N))
+        lin = np.where(np.arange(q)[None, None, :] == y[:, :, None], 0.9, 0.1 / (q - 1))
+        xy = np.log(lin * (0.9 + 0.2 * rng.random(lin.shape)))
+    info, prob, size, ap = sc.QaryListDecoder(q, 1 << n, frozen, L, use_log=True).decode(xy, fv, act)
+    compared = 0
+    for b in range(xy.shape[0]):
+        (k, oinfo, oprob, oap), gap = _oracle_log_with_gap(monkeypatch, q, frozen, L, xy[b], fv[b], act[b])
+        assert size[b] == k
+        if gap < 1e-9:
+            continue
+        compared += 1
+        assert info[b][:k].tolist() == oinfo
+        assert _close_log(prob[b][:k], np.array(oprob)) and _close_log(ap[b], oap)
+    assert compared >= xy.shape[0] // 2
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_gpu_ir_simulation_log_matches_reference(which, capsys):
+    """irSimulation(..., use_log=True) on the GPU log-domain list decoder: the reference log-domain
+    run's frame errors, rate, ProbResults and printed lines."""
+    from polarcub_amd import coding_qary
+    g = load_golden("scl_log")
+    r = g["meta"]["ir"][which]
+    simulate, make_xy = ir_closures_log(r)
+    frozen = set(int(i) for i in np.nonzero(g[r["name"] + "_frozen"])[0])
+    np.random.seed(r["np_seed"])
+    fe, se, rate, prl = coding_qary.irSimulation(r["q"], 1 << r["n"], simulate, make_xy, r["trials"], frozen, r["L"],
+                                                 r["check_size"], use_log=True, verbosity=1)
+    assert fe == r["frame_error_prob"] and rate == r["rate"]
+    assert [p.name for p in prl] == r["prob_results"]
+    assert capsys.readouterr().out.splitlines()[:2] == r["printed"].splitlines()[:2]

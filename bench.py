@@ -225,10 +225,11 @@ class Deletion:
         self.code = sc.CodeSpec.from_frozen_set(self.N, frozen, 200, device=device)
         self.K = self.code.K
         self.dec = sc.DeletionDecoder(self.code, self.n0, self.pd, self.ones)
-        gen = torch.Generator(device=device)
-        gen.manual_seed(mc.shard_seed(a.seed, rank))
-        self.rx, self.rx_len, self.info_tx = mc.deletion_batch(self.code, self.B, self.n0, self.xi, self.pd, gen,
-                                                               ones=self.ones)
+        # Philox keyed by the global codeword index: rank r's shard is codewords [r*B, (r+1)*B) of
+        # the one-GPU run, so sharded counters sum to the single run's
+        info_w, self.rx, self.rx_len = mc.philox_deletion_batch(self.code, a.seed, mc.rank_offset(rank, self.B),
+                                                                self.B, self.n0, self.xi, self.pd, self.ones)
+        self.info_tx = sc.unpack(info_w, self.K)
         self.outs = None
 
     def step(self):
@@ -248,8 +249,8 @@ class Deletion:
             metric="decoded codewords/sec, deletion channel N=%d n0=%d pd=%.2f (main_deletion.py), batch=%d per GPU"
                    % (self.N, self.n0, self.pd, self.B),
             dtype="f64",
-            data="synthetic: uniform info bits, GPU polar encoder, guard bands (xi=%.2f), deletions drawn on device"
-                 % self.xi,
+            data="synthetic: uniform info bits, GPU polar encoder, guard bands (xi=%.2f), deletions drawn on device "
+                 "(Philox keyed by global codeword index)" % self.xi,
             config={"workload": "deletion SC decode N=%d n0=%d K=%d pd=%.2f ones=%d%s"
                                 % (self.N, self.n0, self.K, self.pd, self.ones,
                                    " (BASELINE configs[4])" if self.n == 8 else ""),
@@ -326,9 +327,8 @@ class Qary:
             sc.set_qary_lds(bool(a.qlds))
 
         self.dec = sc.QaryDecoder(self.code)
-        gen = torch.Generator(device=device)
-        gen.manual_seed(mc.shard_seed(a.seed, rank))
-        self.xy, self.info_tx = mc.qsc_batch(self.code, self.B, a.qsc_p, gen)
+        info, self.xy = mc.philox_qsc_batch(self.code, a.seed, mc.rank_offset(rank, self.B), self.B, a.qsc_p)
+        self.info_tx = info.t()
         self.dec.workspace(self.B)
         self.outs = None
 
@@ -350,7 +350,8 @@ class Qary:
             metric="decoded codewords/sec, q=%d SC N=%d QSC(%.2f), batch=%d per GPU" % (self.q, self.N, self.a.qsc_p,
                                                                                      self.B),
             dtype="f64",
-            data="synthetic: uniform info symbols, GPU q-ary encoder, QSC(%.2f) on device" % self.a.qsc_p,
+            data="synthetic: uniform info symbols, GPU q-ary encoder, QSC(%.2f) on device (Philox keyed by global "
+                 "codeword index)" % self.a.qsc_p,
             config={"workload": "q-ary SC decode q=%d N=%d K=%d QSC(%.2f) (BASELINE configs[3])"
                                 % (self.q, self.N, self.K, self.a.qsc_p),
                     "N": self.N, "K": self.K, "q": self.q, "batch_per_gpu": self.B, "frozen_set": self.construction,

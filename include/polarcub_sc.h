@@ -208,6 +208,24 @@ int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int
 int pcub_mc_count_errors(const uint32_t* decoded_words, const uint32_t* sent_words, int64_t B, int32_t K,
                          uint64_t* counters, void* stream);
 size_t pcub_mc_run_bin_workspace(int64_t chunk, int32_t log2N, int32_t K);
+
+/* The q-ary and deletion Monte-Carlo inputs under the same global-index keying (so q-ary and
+ * deletion runs sharded over G GPUs decode the 1-GPU run's codewords and their counters match):
+ *   pcub_mc_info_qary    K uniform symbols in [0, q) per codeword -> [K][B] u8
+ *   pcub_mc_channel_qsc  q-ary codewords [N][B] u8 -> QSC(p) joint rows [N][B][q] f64
+ *                        (makeQSC, ScalarDistributions/QaryMemorylessDistribution.py:780-784)
+ *   pcub_mc_deletion     codeword bits [ceil(N/32)][B] -> the guard-banded word of template tmpl
+ *                        (W entries: >= 0 a codeword bit index, -1 a guard zero, -2 a guard one;
+ *                        Guardbands.addDeletionGuardBands, Guardbands.py:4-44) through the
+ *                        deletion channel (each symbol dropped with probability pd,
+ *                        BinaryTrellis.deletionChannelSimulation, BinaryTrellis.py:441-461):
+ *                        rx [B][W] u8 (survivors left-packed, zero-padded), rx_len [B] i32 */
+int pcub_mc_info_qary(uint64_t seed, int64_t offset, int64_t B, int32_t K, int32_t q, uint8_t* info, void* stream);
+int pcub_mc_channel_qsc(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t q, double p,
+                        const uint8_t* x, double* xy, void* stream);
+int pcub_mc_deletion(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, const int32_t* tmpl, int32_t W,
+                     double pd, const uint32_t* x_words, uint8_t* rx, int32_t* rx_len, void* stream);
+
 int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int32_t log2N, int32_t channel, double param,
                     const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K, int64_t chunk,
                     uint64_t* counters, void* workspace, size_t workspace_bytes, void* stream);

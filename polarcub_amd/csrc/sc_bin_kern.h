@@ -22,7 +22,7 @@ constexpr int kBinBlock = 256;
 struct Variant {
     int S, G, W, L, T, Y, H, P;
 };
-constexpr int kNumVariants = 30;
+constexpr int kNumVariants = 33;
 constexpr Variant kVar[kNumVariants] = {
     {16, 1, 2, 0, 0}, {8, 1, 4, 0, 0}, {32, 1, 1, 0, 0}, {16, 4, 2, 0, 0}, {8, 4, 4, 0, 0}, {16, 2, 2, 0, 0},
     {32, 2, 1, 0, 0}, {8, 8, 4, 0, 0}, {16, 2, 2, 0, 1}, {8, 8, 4, 0, 1}, {16, 4, 2, 0, 1}, {8, 4, 4, 1, 0},
@@ -31,6 +31,7 @@ constexpr Variant kVar[kNumVariants] = {
     {32, 16, 2, 0, 1}, {32, 16, 3, 0, 1}, {16, 16, 3, 0, 1},
     {32, 4, 3, 0, 1, 1}, {32, 8, 3, 0, 1, 1},
     {32, 4, 2, 0, 1, 1, 1, 2}, {32, 4, 2, 0, 1, 1, 1, 1}, {32, 4, 2, 0, 1, 1, 1, 3}, {32, 4, 3, 0, 1, 1, 0, 2},
+    {32, 8, 2, 0, 1, 1, 1, 2}, {32, 4, 2, 0, 1, 0, 1, 2}, {16, 8, 3, 0, 1, 1, 1, 2},
 };
 
 // LDS bytes of the stage level (L: S pairs per thread) or of the split level's LDS half (H: S doubles)
@@ -76,5 +77,6 @@ BinKernFn bin_kernel_part1(int v);
 BinKernFn bin_kernel_part2(int v);
 BinKernFn bin_kernel_part3(int v);
 BinKernFn bin_kernel_part4(int v);
+BinKernFn bin_kernel_part5(int v);
 
 }  // namespace pcub

@@ -75,13 +75,25 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     A.xhat = xhat_words;
     A.leaf = leaf;
     const long long cpb = kDelBlock >> (n - n0);
-    const long long grid = (B + cpb - 1) / cpb;
-    if (grid * kDelBlock > 0xffffffffLL) return PCUB_EINVAL;  // 32-bit dispatch grid (work-items)
+    long long grid = (B + cpb - 1) / cpb;
     // bit-packed received words in LDS when the group's words fit in 32 KiB (always for
     // the 64-trellis shapes; very long padded rows of small codes parse from HBM)
     const long long rw = ((long long)stride + 31) / 32;
     A.rw = (cpb * rw * 4 <= 32768) ? (int)rw : 0;
     const size_t lds = A.rw ? (size_t)(cpb * rw * 4) : 0;
+    // n0 = 2 without ones: each workgroup first builds the segment-state table, so the launch
+    // is persistent (one resident grid striding over the codeword groups)
+    if (n0 == 2 && ones == 0) {
+        int dev = 0, cus = 0, occ = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kDelBlock, lds) == hipSuccess && cus > 0 &&
+            occ > 0) {
+            const long long res = (long long)cus * occ;
+            if (grid > res) grid = res;
+        }
+    }
+    if (grid * kDelBlock > 0xffffffffLL) return PCUB_EINVAL;  // 32-bit dispatch grid (work-items)
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kDelBlock), lds, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }

@@ -440,6 +440,22 @@ __device__ __forceinline__ uint32_t del_n02_half(const Base02& b, const uint32_t
     return (xm ^ xp) | (xp << 1);
 }
 
+// del_n02 through the workgroup's state table (trellis_n02.h: n02_table_entry): the same four
+// subtree inputs in the same order, looked up instead of rebuilt per lane
+template <int T, bool EXP>
+__device__ __forceinline__ uint32_t del_n02_tab(const double* tb, DelCtx<T, EXP>& cx) {
+    const uint32_t xm = cx.subtree(tb[0]);
+    const uint32_t xp = cx.subtree(tb[1 + xm]);
+    const uint32_t ym = (xm ^ xp) | (xp << 1);
+    const uint32_t xm2 = cx.subtree(tb[3 + ym]);
+    const uint32_t xp2 = cx.subtree(tb[7 + 2 * ym + xm2]);
+    const uint32_t yp = (xm2 ^ xp2) | (xp2 << 1);
+    uint32_t x = 0;  // x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h]
+#pragma unroll
+    for (int h = 0; h < 2; ++h) x |= ((((ym ^ yp) >> h) & 1u) << (2 * h)) | (((yp >> h) & 1u) << (2 * h + 1));
+    return x;
+}
+
 template <int T, bool EXP>
 __device__ __forceinline__ uint32_t del_n02(const Base02& b, DelCtx<T, EXP>& cx) {
     const uint32_t ym = del_n02_half(b, nullptr, cx);
@@ -451,20 +467,18 @@ __device__ __forceinline__ uint32_t del_n02(const Base02& b, DelCtx<T, EXP>& cx)
 }
 
 template <int N0, int TB, bool EXP, int OC>
-__global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
+__device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint32_t* xs, const double* n02tab) {
     constexpr int L = 1 << N0;
     constexpr int T = 1 << TB;
     constexpr int CPB = kDelBlock / T;       // codewords per workgroup
     constexpr int NB = T * L;                // code length N
     constexpr int WPC = (NB + 31) / 32;      // x_hat words per codeword
     using Cap = DelCap<L, OC>;
-    static_assert(T <= kDelBlock, "at most one workgroup per codeword");
-    __shared__ uint32_t xs[CPB * WPC];
-
+    constexpr bool TAB = N0 == 2 && OC == 0;
     const int lane = threadIdx.x & 63;
     const int p = threadIdx.x & (T - 1);
     const int g = threadIdx.x >> TB;
-    const long long cw = (long long)blockIdx.x * CPB + g;
+    const long long cw = grp * CPB + g;
     const bool valid = cw < A.B;
     const long long c = valid ? cw : A.B - 1;  // padding groups decode a duplicate, store nothing
     for (int i = threadIdx.x; i < CPB * WPC; i += kDelBlock) xs[i] = 0;
@@ -477,7 +491,7 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
     const bool pk = A.rw > 0;
     if (pk) {
         for (int gg = threadIdx.x >> 6; gg < CPB; gg += kDelBlock / 64) {
-            long long cg = (long long)blockIdx.x * CPB + gg;
+            long long cg = grp * CPB + gg;
             cg = cg < A.B ? cg : A.B - 1;
             const uint8_t* row = A.rx + cg * (long long)A.stride;
             int ln = A.rx_len[cg];
@@ -522,17 +536,12 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
     cx.nacc = 0;
     cx.infow = 0;
     uint32_t x;
-    if constexpr (N0 == 2 && OC == 0) {
-        // register-resident path (trellis_n02.h): the base trellis is implicit
-        Base02 b;
-        b.m = m;
-        b.d = kN02L - m;
-        b.y = 0;
+    if constexpr (TAB) {
+        // the segment's state indexes the workgroup's table (trellis_n02.h, n02_table_entry)
+        uint32_t y = 0;
         if (m <= kN02L)
-            for (int i = 0; i < m; ++i) b.y |= (uint32_t)(bit(s + i) & 1) << i;
-        b.pins = 0.5 * (1.0 - A.pd);
-        b.pdel = 0.5 * A.pd;
-        x = del_n02(b, cx);
+            for (int i = 0; i < m; ++i) y |= (uint32_t)(bit(s + i) & 1) << i;
+        x = del_n02_tab(n02tab + n02_state(m, y) * kN02Row, cx);
     } else if constexpr (N0 >= 3 && OC == 0) {
         x = DelBase<L, T, EXP>::run(base_segment<L>(bit, s, m, A.pd), cx);
     } else {
@@ -549,6 +558,27 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
     __syncthreads();
     if (A.xhat && valid)
         for (int i = p; i < WPC; i += T) A.xhat[(long long)i * A.B + cw] = xs[g * WPC + i];
+    __syncthreads();  // xs / rxb / exchange buffers are reused by the workgroup's next group
+}
+
+template <int N0, int TB, bool EXP, int OC>
+__global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
+    constexpr int T = 1 << TB;
+    constexpr int CPB = kDelBlock / T;                // codewords per workgroup
+    constexpr int WPC = ((T << N0) + 31) / 32;        // x_hat words per codeword
+    static_assert(T <= kDelBlock, "at most one workgroup per codeword");
+    constexpr bool TAB = N0 == 2 && OC == 0;  // the n0 = 2 stage through the state table
+    __shared__ uint32_t xs[CPB * WPC];
+    __shared__ double n02tab[TAB ? kN02States * kN02Row : 1];
+    if constexpr (TAB) {
+        // once per workgroup (the launch is persistent: a workgroup strides over codeword groups)
+        for (int i = threadIdx.x; i < kN02States * 5; i += kDelBlock)
+            n02_table_entry(i / 5, i % 5, A.pd, n02tab + (i / 5) * kN02Row);
+        __syncthreads();
+    }
+    const long long ngrp = (A.B + CPB - 1) / CPB;
+    for (long long grp = blockIdx.x; grp < ngrp; grp += gridDim.x)
+        del_group<N0, TB, EXP, OC>(A, grp, xs, n02tab);
 }
 
 typedef void (*DelKern)(DelArgs);

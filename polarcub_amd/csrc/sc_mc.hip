@@ -173,6 +173,69 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_count(const uint32_t* dec, cons
 
 unsigned grid_of(long long work) { return (unsigned)((work + kMcBlock - 1) / kMcBlock); }
 
+// uniform symbol in [0, m) from 32 random bits (multiply-shift)
+PCUB_HD uint32_t below(uint32_t r, uint32_t m) { return (uint32_t)(((uint64_t)r * m) >> 32); }
+
+// q-ary information symbols [K][B] u8: symbol k of codeword g is below(q) of Philox output
+// lane (k & 3) of counter (g, kStreamInfo, k >> 2)
+__global__ __launch_bounds__(kMcBlock) void k_mc_info_qary(McArgs A, int q, uint8_t* info) {
+    const long long b = (long long)blockIdx.x * kMcBlock + threadIdx.x;
+    if (b >= A.B) return;
+    const uint64_t g = (uint64_t)(A.offset + b);
+    for (int k = 0; k < A.K; k += 4) {
+        const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamInfo, (uint32_t)(k >> 2), (uint32_t)A.seed,
+                            (uint32_t)(A.seed >> 32));
+        for (int j = 0; j < 4 && k + j < A.K; ++j) info[(long long)(k + j) * A.B + b] = (uint8_t)below(r.v[j], q);
+    }
+}
+
+// q-ary symmetric channel (makeQSC, ScalarDistributions/QaryMemorylessDistribution.py:780-784) as
+// joint rows [N][B][q]: position i of codeword g draws counter (g, kStreamChannel, i): words 0-1
+// a 53-bit uniform u (error iff u <= p), word 2 the shift s in [1, q) of an erroneous symbol;
+// y = (x + s) % q, row[y'] = 1 - p if y' == y else p / (q - 1)
+__global__ __launch_bounds__(kMcBlock) void k_mc_qsc(McArgs A, int q, const uint8_t* x, double* xy) {
+    const long long b = (long long)blockIdx.x * kMcBlock + threadIdx.x;
+    if (b >= A.B) return;
+    const uint64_t g = (uint64_t)(A.offset + b);
+    const long long N = 1LL << A.n;
+    const double hit = 1.0 - A.param, miss = A.param / (double)(q - 1);
+    for (long long i = blockIdx.y; i < N; i += gridDim.y) {
+        const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)i, (uint32_t)A.seed,
+                            (uint32_t)(A.seed >> 32));
+        const int xs = x[i * A.B + b];
+        const bool err = u01(r.v[0], r.v[1]) <= A.param;
+        const int y = err ? (xs + 1 + (int)below(r.v[2], q - 1)) % q : xs;
+        double* row = xy + (i * A.B + b) * q;
+        for (int t = 0; t < q; ++t) row[t] = t == y ? hit : miss;
+    }
+}
+
+// Guard bands + deletion channel (Guardbands.addDeletionGuardBands, Guardbands.py:4-44;
+// BinaryTrellis.deletionChannelSimulation, BinaryTrellis.py:441-461): symbol j of the
+// guard-banded word is tmpl[j] >= 0 ? codeword bit tmpl[j] : (tmpl[j] == -2 ? 1 : 0); it survives
+// iff its uniform (32-bit lane (j & 3) of counter (g, kStreamChannel, j >> 2)) is >= pd.  One
+// thread per codeword packs the survivors into its row of rx [B][W].
+__global__ __launch_bounds__(kMcBlock) void k_mc_deletion(McArgs A, const int32_t* tmpl, int W, const uint32_t* x,
+                                                           uint8_t* rx, int32_t* rx_len) {
+    const long long b = (long long)blockIdx.x * kMcBlock + threadIdx.x;
+    if (b >= A.B) return;
+    const uint64_t g = (uint64_t)(A.offset + b);
+    uint8_t* row = rx + b * (long long)W;
+    int o = 0;
+    P4 r{{0, 0, 0, 0}};
+    for (int j = 0; j < W; ++j) {
+        if ((j & 3) == 0)
+            r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)(j >> 2), (uint32_t)A.seed,
+                       (uint32_t)(A.seed >> 32));
+        const double u = ((double)r.v[j & 3] + 0.5) * (1.0 / 4294967296.0);
+        const int t = tmpl[j];
+        const uint8_t v = t >= 0 ? (uint8_t)((x[(long long)(t >> 5) * A.B + b] >> (t & 31)) & 1u) : (uint8_t)(t == -2);
+        if (u >= A.param) row[o++] = v;
+    }
+    for (int j = o; j < W; ++j) row[j] = 0;
+    rx_len[b] = o;
+}
+
 }  // namespace
 
 extern "C" int pcub_mc_info(uint64_t seed, int64_t offset, int64_t B, int32_t K, uint32_t* info_words, void* stream) {
@@ -205,6 +268,44 @@ extern "C" int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t
     if (gx > 0x7fffffffLL) return PCUB_EINVAL;
     hipLaunchKernelGGL(k_mc_channel, dim3((unsigned)gx, (unsigned)gy), dim3(kMcBlock), 0, (hipStream_t)stream, A,
                        x_words, (double2*)xy);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcub_mc_info_qary(uint64_t seed, int64_t offset, int64_t B, int32_t K, int32_t q, uint8_t* info,
+                                 void* stream) {
+    if (B < 0 || offset < 0 || K < 0 || q < 2 || q > 255 || (K > 0 && B > 0 && !info)) return PCUB_EINVAL;
+    if (B == 0 || K == 0) return 0;
+    McArgs A{seed, offset, B, 0, K, 0, 0.0, 0.0, 0.0, 0.0};
+    hipLaunchKernelGGL(k_mc_info_qary, dim3(grid_of(B)), dim3(kMcBlock), 0, (hipStream_t)stream, A, (int)q, info);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcub_mc_channel_qsc(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t q, double p,
+                                   const uint8_t* x, double* xy, void* stream) {
+    if (B < 0 || offset < 0 || log2N < 0 || log2N > 24 || q < 2 || q > 255 || !(p >= 0.0 && p <= 1.0))
+        return PCUB_EINVAL;
+    if (B == 0) return 0;
+    if (!x || !xy) return PCUB_EINVAL;
+    McArgs A{seed, offset, B, log2N, 0, 2, p, 0.0, 0.0, 0.0};
+    const long long gx = (B + kMcBlock - 1) / kMcBlock;
+    long long gy = (16384 + gx - 1) / gx;
+    if (gy > ((long long)1 << log2N)) gy = (long long)1 << log2N;
+    if (gy > 65535) gy = 65535;
+    if (gx > 0x7fffffffLL) return PCUB_EINVAL;
+    hipLaunchKernelGGL(k_mc_qsc, dim3((unsigned)gx, (unsigned)gy), dim3(kMcBlock), 0, (hipStream_t)stream, A, (int)q,
+                       x, xy);
+    return (int)hipGetLastError();
+}
+
+extern "C" int pcub_mc_deletion(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, const int32_t* tmpl,
+                                int32_t W, double pd, const uint32_t* x_words, uint8_t* rx, int32_t* rx_len,
+                                void* stream) {
+    if (B < 0 || offset < 0 || log2N < 0 || log2N > 24 || W < 0 || !(pd >= 0.0 && pd <= 1.0)) return PCUB_EINVAL;
+    if (B == 0) return 0;
+    if (!tmpl || !x_words || !rx || !rx_len) return PCUB_EINVAL;
+    McArgs A{seed, offset, B, log2N, 0, 3, pd, 0.0, 0.0, 0.0};
+    hipLaunchKernelGGL(k_mc_deletion, dim3(grid_of(B)), dim3(kMcBlock), 0, (hipStream_t)stream, A, tmpl, (int)W,
+                       x_words, rx, rx_len);
     return (int)hipGetLastError();
 }
 

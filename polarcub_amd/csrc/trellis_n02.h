@@ -313,4 +313,49 @@ PCUB_HD void n02_collapse_paths(const Paths02& q, const uint32_t* dec, double& m
     }
 }
 
+// The whole n0 = 2 trellis stage of one lane is a function of its segment alone: the base
+// trellis follows from (m, y, pd), and every value the lane hands to the memoryless subtree
+// is a collapse of a child built from it under the decisions made so far.  So the four values
+// a lane produces per codeword -- v1 = collapse(minus child), v2[xm] = collapse(minus child,
+// xm), v3[ym] = collapse(plus child under ym), v4[ym][xm'] -- take one of 15 values per segment
+// state, and there are 32 states: (m, y) for m <= 4 (index 2^m - 1 + y) and "no edges" (m > 4,
+// index 31).  n02_table_entry computes one (state, child) row of that table with the same
+// functions, in the same order, as the per-lane path (so the values are identical).
+constexpr int kN02States = 32;
+constexpr int kN02Row = 16;  // 15 values per state, padded
+
+PCUB_HD int n02_state(int m, uint32_t y) { return (m >= 0 && m <= kN02L) ? (1 << m) - 1 + (int)y : kN02States - 1; }
+
+// child cv of state st (cv 0: the minus child; cv 1..4: the plus child under ym = cv - 1) into
+// row[0..14]: [0] = v1, [1 + xm] = v2, [3 + ym] = v3, [7 + 2 ym + xm'] = v4
+PCUB_HD void n02_table_entry(int st, int cv, double pd, double* row) {
+    Base02 b;
+    if (st == kN02States - 1) {
+        b.m = kN02L + 1;
+        b.y = 0;
+    } else {
+        int m = 0;
+        while ((2 << m) <= st + 1) ++m;
+        b.m = m;
+        b.y = (uint32_t)(st + 1 - (1 << m));
+    }
+    b.d = kN02L - b.m;
+    b.pins = 0.5 * (1.0 - pd);
+    b.pdel = 0.5 * pd;
+    const uint32_t ym = (uint32_t)(cv - 1);
+    Child02 c;
+    n02_transform(b, cv ? &ym : nullptr, c);
+    n02_normalize(c);
+    Paths02 q;
+    n02_paths(c, q);
+    double m0, m1;
+    n02_collapse_paths(q, nullptr, m0, m1);
+    row[cv ? 3 + (int)ym : 0] = norm_pack(m0, m1);
+#pragma unroll
+    for (uint32_t xb = 0; xb < 2; ++xb) {
+        n02_collapse_paths(q, &xb, m0, m1);
+        row[cv ? 7 + 2 * (int)ym + (int)xb : 1 + (int)xb] = norm_pack(m0, m1);
+    }
+}
+
 }  // namespace pcub

@@ -157,3 +157,59 @@ def run_bin(code, seed, offset, count, channel, param, chunk=1 << 18):
                            ws.numel(), sc._stream())
     _lib.check(rc, "pcub_mc_run_bin")
     return [int(v) for v in counters.tolist()]
+
+
+def philox_qsc_batch(code, seed, offset, B, p):
+    """q-ary information [K, B] u8 and QSC(p) joint rows [N, B, q] for global codewords
+    [offset, offset + B) (pcub_mc_info_qary -> pcub_polar_encode_qary -> pcub_mc_channel_qsc);
+    the same codewords whichever rank or chunk generates them."""
+    from . import _lib
+    L = _lib.lib()
+    dev = code.device
+    info = torch.zeros((max(1, code.K), B), dtype=torch.uint8, device=dev)
+    _lib.check(L.pcub_mc_info_qary(int(seed), int(offset), B, code.K, code.q, sc._p(info), sc._stream()),
+               "pcub_mc_info_qary")
+    x = torch.empty((code.N, B), dtype=torch.uint8, device=dev)
+    _lib.check(L.pcub_polar_encode_qary(sc._p(info), B, code.n, code.q, sc._p(code.frozen_dev), code.K, sc._p(x),
+                                        sc._stream()), "pcub_polar_encode_qary")
+    xy = torch.empty((code.N, B, code.q), dtype=torch.float64, device=dev)
+    _lib.check(L.pcub_mc_channel_qsc(int(seed), int(offset), B, code.n, code.q, float(p), sc._p(x), sc._p(xy),
+                                     sc._stream()), "pcub_mc_channel_qsc")
+    return info[:code.K], xy
+
+
+_TEMPLATES = {}
+
+
+def guard_template(n, n0, xi, ones, device):
+    """The guard-banded word's template for pcub_mc_deletion (codeword bit index, -1 zero, -2 one)."""
+    key = (n, n0, float(xi), ones, str(device))
+    t = _TEMPLATES.get(key)
+    if t is None:
+        pos, W, ones_pos = channel.guard_band_positions(n, n0, xi, ones)
+        a = [-1] * W
+        for i, j in enumerate(pos):
+            a[j] = i
+        for j in ones_pos:
+            a[j] = -2
+        t = _TEMPLATES[key] = torch.tensor(a, dtype=torch.int32, device=device)
+    return t
+
+
+def philox_deletion_batch(code, seed, offset, B, n0, xi, pd, ones=0):
+    """Information words [ceil(K/32), B], received words rx [B, W] u8 and rx_len [B] i32 for global
+    codewords [offset, offset + B): pcub_mc_info -> pcub_polar_encode_bin -> guard bands ->
+    pcub_mc_deletion."""
+    from . import _lib
+    L = _lib.lib()
+    dev = code.device
+    info = torch.zeros((max(1, code.info_words), B), dtype=torch.int32, device=dev)
+    _lib.check(L.pcub_mc_info(int(seed), int(offset), B, code.K, sc._p(info), sc._stream()), "pcub_mc_info")
+    x = sc.encode_native(code, info)
+    t = guard_template(code.n, n0, xi, ones, dev)
+    W = int(t.numel())
+    rx = torch.empty((B, W), dtype=torch.uint8, device=dev)
+    ln = torch.empty(B, dtype=torch.int32, device=dev)
+    _lib.check(L.pcub_mc_deletion(int(seed), int(offset), B, code.n, sc._p(t), W, float(pd), sc._p(x), sc._p(rx),
+                                  sc._p(ln), sc._stream()), "pcub_mc_deletion")
+    return info, rx, ln

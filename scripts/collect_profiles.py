@@ -124,6 +124,10 @@ def main():
         summ["valu_active_per_wave_cycle"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
     if "SQ_INSTS_VALU" in avg and "SQ_WAVES" in avg:
         summ["valu_insts_per_wave"] = avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
+    summ["counters_per_codeword"] = {k: v / a.batch for k, v in avg.items()
+                                     if k.startswith("SQ_INSTS") or k in ("SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES")}
+    if "GRBM_GUI_ACTIVE" in avg and "SQ_BUSY_CYCLES" not in avg:
+        summ["gpu_active_cycles"] = avg["GRBM_GUI_ACTIVE"]
     if a.bench and os.path.exists(os.path.join(root, a.bench)):
         shutil.copy(os.path.join(root, a.bench), os.path.join(dst, "bench.json"))
     with open(os.path.join(dst, "summary.json"), "w") as f:

@@ -180,6 +180,14 @@ std::vector<uint32_t> decode_n02(const BitF& bit, int len, int tb, double pd, Ct
         b[t].pins = 0.5 * (1.0 - pd);
         b[t].pdel = 0.5 * pd;
     }
+    // the kernel's per-workgroup segment-state table (n02_table_entry): every value below must
+    // equal its table entry bit for bit
+    std::vector<double> tab(kN02States * kN02Row, 0.0);
+    for (int st = 0; st < kN02States; ++st)
+        for (int cv = 0; cv < 5; ++cv) n02_table_entry(st, cv, pd, tab.data() + st * kN02Row);
+    auto check_tab = [&](int t, int k, double v) {
+        if (as_bits(tab[n02_state(b[t].m, b[t].y) * kN02Row + k]) != as_bits(v)) throw 6;
+    };
     std::vector<Child02> c(T);
     std::vector<uint32_t> y[2];
     std::vector<double> vals(T);
@@ -199,6 +207,7 @@ std::vector<uint32_t> decode_n02(const BitF& bit, int len, int tb, double pd, Ct
             double m0, m1;
             collapse(c[t], nullptr, m0, m1);
             vals[t] = norm_pack(m0, m1);
+            check_tab(t, half ? 3 + (int)y[0][t] : 0, vals[t]);
         }
         const std::vector<int> xm = mem_sc(vals, cx);
         for (int t = 0; t < T; ++t) {
@@ -206,6 +215,7 @@ std::vector<uint32_t> decode_n02(const BitF& bit, int len, int tb, double pd, Ct
             const uint32_t d = (uint32_t)xm[t];
             collapse(c[t], &d, m0, m1);
             vals[t] = norm_pack(m0, m1);
+            check_tab(t, half ? 7 + 2 * (int)y[0][t] + xm[t] : 1 + xm[t], vals[t]);
         }
         const std::vector<int> xp = mem_sc(vals, cx);
         y[half].resize(T);

@@ -116,3 +116,104 @@ def test_bsc_channel_law(code):
     for half in (flips[0::2], flips[1::2]):
         f = half.mean()
         assert abs(f - p) < 5 * math.sqrt(p * (1 - p) / half.size)
+
+
+# -- q-ary and deletion inputs keyed by the global codeword index --------------------------------
+
+@pytest.fixture(scope="module")
+def qcode():
+    from polarcub_amd import sc
+    g = load_golden("construct_qary")
+    return sc.QaryCode(4, 256, g["qsc4_n8_L64_frozen"].astype(np.uint8), device="cuda")
+
+
+def test_qsc_batches_keyed_by_global_index(qcode):
+    from polarcub_amd import mc
+    info_a, xy_a = mc.philox_qsc_batch(qcode, 5, 1000, 300, 0.11)
+    info_b, xy_b = mc.philox_qsc_batch(qcode, 5, 1100, 50, 0.11)
+    assert torch.equal(info_a[:, 100:150], info_b) and torch.equal(xy_a[:, 100:150], xy_b)
+    info_c, _ = mc.philox_qsc_batch(qcode, 6, 1100, 50, 0.11)
+    assert not torch.equal(info_b, info_c)
+
+
+def test_qsc_channel_law(qcode):
+    """Symbols uniform on Z_q; a position is in error with probability p, its wrong symbol
+    uniform over the q - 1 others; rows are makeQSC's table."""
+    from polarcub_amd import mc, sc
+    B, p, q = 1 << 14, 0.11, 4
+    info, xy = mc.philox_qsc_batch(qcode, 9, 0, B, p)
+    counts = torch.bincount(info.reshape(-1).long(), minlength=q).double()
+    assert torch.all((counts / counts.sum() - 1 / q).abs() < 5e-3)
+    x = sc.encode_qary(qcode, info.t().contiguous()).t()  # [N, B]
+    y = xy.argmax(dim=2)
+    assert torch.all((xy.max(dim=2).values == 1 - p)) and torch.all(xy.sum(dim=2).sub(1.0).abs() < 1e-12)
+    err = (y != x.long())
+    rate = err.double().mean().item()
+    n = err.numel()
+    assert abs(rate - p) < 5 * math.sqrt(p * (1 - p) / n)
+    shift = ((y - x.long()) % q)[err]
+    sc_ = torch.bincount(shift, minlength=q).double()[1:]
+    assert torch.all((sc_ / sc_.sum() - 1 / (q - 1)).abs() < 0.01)
+
+
+def test_qsc_sharded_counters_match_single_run(qcode):
+    """q-ary decode over [0, 2B) in one batch and in two shards: identical frame / symbol errors."""
+    from polarcub_amd import mc, sc
+    B = 4096
+    dec = sc.QaryDecoder(qcode)
+
+    def run(off, b):
+        info, xy = mc.philox_qsc_batch(qcode, 21, off, b, 0.11)
+        out = dec.decode_native(xy)
+        return mc.error_counts(out[0].t(), info.t())
+    one = run(0, 2 * B)
+    a, b = run(0, B), run(B, B)
+    assert one == (a[0] + b[0], a[1] + b[1]) and one[0] > 0
+
+
+@pytest.fixture(scope="module")
+def dcode():
+    from polarcub_amd import construction, sc
+    N = 256
+    fr = construction.bhattacharyya_frozen(8, 64, 0.5)
+    return sc.CodeSpec.from_frozen_set(N, set(np.nonzero(fr)[0].tolist()), 200, device="cuda")
+
+
+def test_deletion_batches_keyed_by_global_index(dcode):
+    from polarcub_amd import mc
+    ia, ra, la = mc.philox_deletion_batch(dcode, 3, 500, 200, 2, 0.1, 0.1)
+    ib, rb, lb = mc.philox_deletion_batch(dcode, 3, 550, 40, 2, 0.1, 0.1)
+    assert torch.equal(ia[:, 50:90], ib) and torch.equal(ra[50:90], rb) and torch.equal(la[50:90], lb)
+
+
+@pytest.mark.parametrize("ones", [0, 2])
+def test_deletion_channel_law(dcode, ones):
+    """pd = 0 gives the guard-banded codeword itself (Guardbands.addDeletionGuardBands of the
+    GPU-encoded word); pd > 0 keeps each symbol with probability 1 - pd."""
+    from polarcub_amd import deletion, mc, sc
+    B = 2048
+    info_w, rx, ln = mc.philox_deletion_batch(dcode, 11, 0, B, 2, 0.1, 0.0, ones)
+    x = sc.unpack(sc.encode_native(dcode, info_w), dcode.N).cpu().numpy()
+    for b in (0, 1, B - 1):
+        want = deletion.addDeletionGuardBands([int(v) for v in x[b]], 8, 2, 0.1, ones)
+        assert int(ln[b]) == len(want) and rx[b, :len(want)].cpu().tolist() == list(want)
+    pd = 0.1
+    _, rx, ln = mc.philox_deletion_batch(dcode, 12, 0, B, 2, 0.1, pd, ones)
+    W = rx.shape[1]
+    kept = ln.double().sum().item() / (B * W)
+    assert abs(kept - (1 - pd)) < 5 * math.sqrt(pd * (1 - pd) / (B * W))
+    assert torch.all(rx[torch.arange(W, device="cuda")[None, :] >= ln[:, None]] == 0)
+
+
+def test_deletion_sharded_counters_match_single_run(dcode):
+    from polarcub_amd import mc, sc
+    dec = sc.DeletionDecoder(dcode, 2, 0.1)
+    B = 2048
+
+    def run(off, b):
+        info_w, rx, ln = mc.philox_deletion_batch(dcode, 31, off, b, 2, 0.1, 0.1)
+        iw, _ = dec.decode_native(rx, ln)
+        return mc.error_counts(sc.unpack(iw, dcode.K), sc.unpack(info_w, dcode.K))
+    one = run(0, 2 * B)
+    a, b = run(0, B), run(B, B)
+    assert one == (a[0] + b[0], a[1] + b[1]) and one[0] > 0

@@ -29,7 +29,7 @@ def lib():
     if _lib is not None:
         return _lib
     path = _build.LIB
-    if not os.path.exists(path) or not _build.up_to_date():
+    if not _build.lib_current():
         _build.build()
     L = ctypes.CDLL(path)
     L.pcub_abi_version.restype = ctypes.c_int
@@ -48,6 +48,8 @@ def lib():
     L.pcub_sc_set_qary_regs.argtypes = [ctypes.c_int]
     L.pcub_sc_set_qary_lds.restype = ctypes.c_int
     L.pcub_sc_set_qary_lds.argtypes = [ctypes.c_int]
+    L.pcub_sc_set_qary_hl.restype = ctypes.c_int
+    L.pcub_sc_set_qary_hl.argtypes = [ctypes.c_int]
     L.pcub_sc_num_variants.restype = ctypes.c_int
     L.pcub_sc_num_variants.argtypes = []
     L.pcub_sc_variant_info.restype = ctypes.c_int

@@ -124,6 +124,12 @@ def _lib_digest():
     return hashlib.sha256("".join(_obj_digest(s) for s in SOURCES).encode()).hexdigest()
 
 
+def lib_current():
+    """True when the library's stamp matches the current sources, headers and flags (its objects
+    need not be present: they stay on the build host)."""
+    return os.path.exists(LIB) and not _stale(LIB, _lib_digest())
+
+
 def up_to_date():
     """True when every object and the library match the current sources, headers and flags."""
     if any(_stale(_obj(s), _obj_digest(s)) for s in SOURCES):

@@ -72,18 +72,25 @@ int g_qlanes = 4;  // requested lanes per codeword (pcub_sc_set_qary_lanes)
 int g_qylds = 1;   // symbols in LDS where a twin kernel exists and fits (pcub_sc_set_qary_lds)
 constexpr size_t kQLdsPerCu = 160 * 1024;
 int g_qregs = 0;   // cap on register positions per lane (pcub_sc_set_qary_regs; 0 = the default)
+int g_qhl = 1;     // split last level (HL twin) where one exists and fits (pcub_sc_set_qary_hl)
 
 // register positions per lane S and lanes per codeword G for a code of 2^n:
 // S = 8 (q <= 4) or 4, G = the requested lanes, both reduced until N >= 2*S*G
 struct QGeom {
     int S, G;
     bool yl;  // symbols in LDS
+    bool hl;  // split last level: 2S positions per lane at the chain's end, S of them in LDS
+    int sr() const { return hl ? 2 * S : S; }
 };
 
 // LDS bytes of a workgroup's symbols: Nv/4 words per thread
 size_t qsym_lds_bytes(int n, int G) { return (size_t)kQBlock * ((((size_t)1 << n) / G + 3) / 4) * sizeof(uint32_t); }
+// LDS bytes of the split level's LDS half: S positions x q doubles per thread
+size_t qhl_lds_bytes(int q, int S) { return (size_t)kQBlock * S * q * sizeof(double); }
+constexpr int kQHlWaves = 3;  // the HL kernels' launch bounds
+
 QGeom q_geom(int q, int n) {
-    QGeom c{4, g_qlanes, false};  // 8 register positions (q <= 4) via pcub_sc_set_qary_regs
+    QGeom c{4, g_qlanes, false, false};  // 8 register positions (q <= 4) via pcub_sc_set_qary_regs
     if (g_qregs > 0) c.S = (q <= 4 || g_qregs <= 4) ? g_qregs : 4;
     while (c.G > 1 && (1 << n) < 2 * c.S * c.G) c.G >>= 1;
     while (c.S > 1 && (1 << n) < 2 * c.S * c.G) c.S >>= 1;
@@ -95,18 +102,23 @@ QGeom q_geom(int q, int n) {
     // symbols in LDS while the resident workgroups' columns fit the CU's LDS (N <= 512 at G = 4)
     c.yl = g_qylds && qary_kernel_y(q, c.S, c.G) &&
            (size_t)qary_waves(q, c.S, c.G) * qsym_lds_bytes(n, c.G) <= kQLdsPerCu;
+    // the split level (with the symbols in LDS) where its three workgroups fit a CU and the code
+    // has an outer level above it (N >= 4 S G)
+    c.hl = c.yl && g_qhl && qary_kernel_h(q, c.S, c.G) && (1 << n) >= 4 * c.S * c.G &&
+           (size_t)kQHlWaves * (qsym_lds_bytes(n, c.G) + qhl_lds_bytes(q, c.S)) <= kQLdsPerCu;
     return c;
 }
 
 QKern qkernel(int q, int n, int* waves = nullptr) {
     const QGeom c = q_geom(q, n);
-    if (waves) *waves = qary_waves(q, c.S, c.G);
+    if (waves) *waves = c.hl ? kQHlWaves : qary_waves(q, c.S, c.G);
+    if (c.hl) return qary_kernel_h(q, c.S, c.G);
     return c.yl ? qary_kernel_y(q, c.S, c.G) : qary_kernel(q, c.S, c.G);
 }
 
 size_t qlaunch_lds(int q, int n) {
     const QGeom c = q_geom(q, n);
-    return c.yl ? qsym_lds_bytes(n, c.G) : 0;
+    return (c.yl ? qsym_lds_bytes(n, c.G) : 0) + (c.hl ? qhl_lds_bytes(q, c.S) : 0);
 }
 
 long long qgrid(long long B, int q, int n) {
@@ -130,17 +142,17 @@ long long qgrid(long long B, int q, int n) {
     return (ntiles + rounds - 1) / rounds;
 }
 
-// per lane: virtual stage levels 1..D-1 (Nv - 2S positions as pairs) + Nv symbol bytes in words
-// (unless the symbols are in LDS)
+// per lane: virtual stage levels 1..D-1 (Nv - 2 SR positions as pairs, SR = the chain-end
+// level's positions) + Nv symbol bytes in words (unless the symbols are in LDS)
 size_t qslot_bytes(int n, int q) {
     const QGeom c = q_geom(q, n);
     const size_t Nv = ((size_t)1 << n) / c.G;
-    return (Nv - 2 * c.S) * (size_t)((q + 1) / 2) * sizeof(double2) + (c.yl ? 0 : ((Nv + 3) & ~(size_t)3));
+    return (Nv - 2 * c.sr()) * (size_t)((q + 1) / 2) * sizeof(double2) + (c.yl ? 0 : ((Nv + 3) & ~(size_t)3));
 }
 
 int q_depth(int n, int q) {
     const QGeom c = q_geom(q, n);
-    return n - __builtin_ctz((unsigned)(c.S * c.G));
+    return n - __builtin_ctz((unsigned)(c.sr() * c.G));
 }
 
 // rate-0 table + packed frozen words, ahead of the slots
@@ -177,7 +189,7 @@ extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, i
     hipLaunchKernelGGL(k_q_frozen_words, dim3((unsigned)(((N + 31) / 32 + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0, st,
                        frozen, N, words);
     hipLaunchKernelGGL(k_q_ef, dim3((unsigned)(((1 << D) + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0, st, words, D,
-                       c.S * c.G, ef);
+                       c.sr() * c.G, ef);
     QArgs A;
     A.xy = xy;
     A.B = B;
@@ -187,9 +199,10 @@ extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, i
     A.info = info;
     A.xhat = xhat;
     A.nslots = g * kQBlock;
+    A.ylds_words = c.yl ? (int)(qsym_lds_bytes(log2N, c.G) / kQBlock / sizeof(uint32_t)) : 0;
     char* slots = (char*)workspace + tb;
     A.scratch = (double2*)slots;
-    A.ysym = c.yl ? nullptr : (uint32_t*)(slots + (size_t)A.nslots * (N / c.G - 2 * c.S) * ((q + 1) / 2) * sizeof(double2));
+    A.ysym = c.yl ? nullptr : (uint32_t*)(slots + (size_t)A.nslots * (N / c.G - 2 * c.sr()) * ((q + 1) / 2) * sizeof(double2));
     hipLaunchKernelGGL(qkernel(q, log2N), dim3((unsigned)g), dim3(kQBlock), qlaunch_lds(q, log2N), st, A);
     return (int)hipGetLastError();
 }
@@ -220,6 +233,15 @@ extern "C" int pcub_sc_set_qary_lds(int on) {
     if (on != 0 && on != 1) return PCUB_EINVAL;
     const int old = g_qylds;
     g_qylds = on;
+    return old;
+}
+
+// Tuning hook (not part of the stable ABI): the split last level (q = 4 HL kernel, three waves)
+// where it exists and fits (1, the default) or not (0).  Returns the previous value.
+extern "C" int pcub_sc_set_qary_hl(int on) {
+    if (on != 0 && on != 1) return PCUB_EINVAL;
+    const int old = g_qhl;
+    g_qhl = on;
     return old;
 }
 

@@ -147,6 +147,7 @@ struct QArgs {
     double2* scratch;        // [(N/G - 2S) positions][ceil(Q/2)][nslots]
     uint32_t* ysym;          // [N/G/4 words][nslots], symbol of position p in byte p % 4 of word p / 4
     long long nslots;
+    int ylds_words;          // symbol words per thread in LDS (YL kernels; the HL column follows them)
 };
 
 // Re-encoded symbols, four per word.  SWAR on bytes: every byte holds a value
@@ -366,6 +367,65 @@ PCUB_HD void q_final(const QPass& P, QV<Q>* v) {
     for (int c = 0; c < S; ++c) v[c] = QCol<Q, F, F, 0, GOP, ROOT, true, YL>::run(P, c, S);
 }
 
+// Final pass of a split-level (HL) chain: the 2S positions of level D, the first S into this
+// thread's LDS column hl (component x of position c at hl[(c * Q + x) * kQHlStride]), the
+// last S into registers.
+constexpr int kQHlStride = 256;  // threads per workgroup (kQaryBlock)
+
+template <int Q, int S, int F, bool GOP, bool ROOT, bool YL>
+PCUB_HD void q_final_hl(const QPass& P, QV<Q>* v, double* hl) {
+#pragma unroll
+    for (int c = 0; c < 2 * S; ++c) {
+        const QV<Q> x = QCol<Q, F, F, 0, GOP, ROOT, true, YL>::run(P, c, 2 * S);
+        if (c < S) {
+#pragma unroll
+            for (int t = 0; t < Q; ++t) hl[(c * Q + t) * kQHlStride] = x.p[t];
+        } else {
+            v[c - S] = x;
+        }
+    }
+}
+
+template <int Q>
+PCUB_HD QV<Q> q_hl_load(const double* hl, int c) {
+    QV<Q> v;
+#pragma unroll
+    for (int t = 0; t < Q; ++t) v.p[t] = hl[(c * Q + t) * kQHlStride];
+    return v;
+}
+
+// The split level's node: 2S positions per lane, the first S in the LDS column, the last S in
+// registers (QSub<Q, 2S, G>'s top node with its parent split); a child whose u range is all
+// frozen is not evaluated (symbols 0, as the rate-0 chains).
+template <int Q, int S, int G>
+PCUB_HD void q_hl_run(const double* hl, const QV<Q>* vr, uint8_t* y, QInfo& qi, int lane) {
+    constexpr int SH = S * G;  // u positions per child
+    constexpr uint64_t HM = (SH == 64) ? ~0ull : ((1ull << SH) - 1ull);
+    QV<Q> c[S];
+    uint8_t ym[S], yp[S];
+    if ((qi.fm & HM) == HM) {
+#pragma unroll
+        for (int t = 0; t < S; ++t) ym[t] = 0;
+    } else {
+#pragma unroll
+        for (int t = 0; t < S; ++t) c[t] = q_minus<Q>(q_hl_load<Q>(hl, t), vr[t]);
+        QSub<Q, S, G>::run(c, ym, 0, qi, lane);
+    }
+    if (((qi.fm >> SH) & HM) == HM) {
+#pragma unroll
+        for (int t = 0; t < S; ++t) yp[t] = 0;
+    } else {
+#pragma unroll
+        for (int t = 0; t < S; ++t) c[t] = q_plus<Q>(q_hl_load<Q>(hl, t), vr[t], ym[t]);
+        QSub<Q, S, G>::run(c, yp, S, qi, lane);
+    }
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+        y[t] = (uint8_t)((ym[t] + yp[t]) % Q);
+        y[t + S] = (uint8_t)((Q - yp[t]) % Q);
+    }
+}
+
 template <int Q, int F, int U, bool YL>
 PCUB_HD void q_pass_dispatch(const QPass& P, int La, bool gop, bool root) {
     if (root) {
@@ -377,14 +437,24 @@ PCUB_HD void q_pass_dispatch(const QPass& P, int La, bool gop, bool root) {
     }
 }
 
-template <int Q, int S, int F, bool YL>
-PCUB_HD void q_final_dispatch(const QPass& P, QV<Q>* v, bool gop, bool root) {
-    if (root) {
-        if (gop) q_final<Q, S, F, true, true, YL>(P, v);
-        else q_final<Q, S, F, false, true, YL>(P, v);
+template <int Q, int S, int F, bool YL, bool HL = false>
+PCUB_HD void q_final_dispatch(const QPass& P, QV<Q>* v, bool gop, bool root, double* hl = nullptr) {
+    if constexpr (HL) {
+        if (root) {
+            if (gop) q_final_hl<Q, S, F, true, true, YL>(P, v, hl);
+            else q_final_hl<Q, S, F, false, true, YL>(P, v, hl);
+        } else {
+            if (gop) q_final_hl<Q, S, F, true, false, YL>(P, v, hl);
+            else q_final_hl<Q, S, F, false, false, YL>(P, v, hl);
+        }
     } else {
-        if (gop) q_final<Q, S, F, true, false, YL>(P, v);
-        else q_final<Q, S, F, false, false, YL>(P, v);
+        if (root) {
+            if (gop) q_final<Q, S, F, true, true, YL>(P, v);
+            else q_final<Q, S, F, false, true, YL>(P, v);
+        } else {
+            if (gop) q_final<Q, S, F, true, false, YL>(P, v);
+            else q_final<Q, S, F, false, false, YL>(P, v);
+        }
     }
 }
 
@@ -394,12 +464,16 @@ PCUB_HD void q_final_dispatch(const QPass& P, QV<Q>* v, bool gop, bool root) {
 // stored stage level fewer each) at the price of duplicated work in the cross-lane
 // leaf levels (both lanes of an exchanging pair evaluate the same transform).
 // YL: the symbols in LDS (ylds = this thread's column, word w at ylds[w * ystride])
-template <int Q, int S, int G = 1, int U = 1, bool YL = false>
+// HL: the chain ends at a split level of 2S positions per lane (the first S in the LDS column
+//     hl, the rest in registers; q_hl_run): one stored stage depth fewer (8qN bytes written and
+//     8qN read less per codeword)
+template <int Q, int S, int G = 1, int U = 1, bool YL = false, bool HL = false>
 PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store, int j = 0, int lane = 0,
-                            uint32_t* ylds = nullptr, long long ystride = 0) {
-    constexpr int s = (S == 1) ? 0 : (S == 2) ? 1 : (S == 4) ? 2 : (S == 8) ? 3 : 4;
+                            uint32_t* ylds = nullptr, long long ystride = 0, double* hl = nullptr) {
+    constexpr int SR = HL ? 2 * S : S;  // positions per lane at the chain's last level
+    constexpr int s = (SR == 1) ? 0 : (SR == 2) ? 1 : (SR == 4) ? 2 : (SR == 8) ? 3 : (SR == 16) ? 4 : 5;
     constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : (G == 4) ? 2 : (G == 8) ? 3 : 4;
-    constexpr int SU = S * G;  // real u positions per register subtree
+    constexpr int SU = SR * G;  // real u positions per chain-end subtree
     constexpr int QP = (Q + 1) / 2;
     static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per codeword");
     static_assert(SU <= 64, "a register subtree's frozen bits fit one 64-bit word");
@@ -450,33 +524,35 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
             a += F;
             gop = false;
         }
-        uint8_t y[S];
+        uint8_t y[SR];
         if (stop == D) {
             QV<Q> v[S];
             const int F = D - a;
-            if (F == 3) q_final_dispatch<Q, S, 3, YL>(P, v, gop, a == 0);
-            else if (F == 2) q_final_dispatch<Q, S, 2, YL>(P, v, gop, a == 0);
-            else q_final_dispatch<Q, S, 1, YL>(P, v, gop, a == 0);
+            if (F == 3) q_final_dispatch<Q, S, 3, YL, HL>(P, v, gop, a == 0, hl);
+            else if (F == 2) q_final_dispatch<Q, S, 2, YL, HL>(P, v, gop, a == 0, hl);
+            else q_final_dispatch<Q, S, 1, YL, HL>(P, v, gop, a == 0, hl);
             const int us = k * SU;
             if constexpr (SU == 64) qi.fm = (uint64_t)A.fwords[us >> 5] | ((uint64_t)A.fwords[(us >> 5) + 1] << 32);
+            else if constexpr (SU == 32) qi.fm = (uint64_t)A.fwords[us >> 5];
             else qi.fm = (uint64_t)(A.fwords[us >> 5] >> (us & 31));
-            QSub<Q, S, G>::run(v, y, 0, qi, lane);
+            if constexpr (HL) q_hl_run<Q, S, G>(hl, v, y, qi, lane);
+            else QSub<Q, S, G>::run(v, y, 0, qi, lane);
         } else {
 #pragma unroll
-            for (int t = 0; t < S; ++t) y[t] = 0;  // rate-0: symbols 0, re-encoding 0
+            for (int t = 0; t < SR; ++t) y[t] = 0;  // rate-0: symbols 0, re-encoding 0
         }
-        // the subtree's symbols into its words (S < 4: a part of one word)
-        if constexpr (S >= 4) {
+        // the subtree's symbols into its words (SR < 4: a part of one word)
+        if constexpr (SR >= 4) {
 #pragma unroll
-            for (int w = 0; w < S / 4; ++w)
-                sty<YL>(Y + (long long)(k * S / 4 + w) * ys, (uint32_t)y[4 * w] | ((uint32_t)y[4 * w + 1] << 8) |
-                                                             ((uint32_t)y[4 * w + 2] << 16) | ((uint32_t)y[4 * w + 3] << 24));
+            for (int w = 0; w < SR / 4; ++w)
+                sty<YL>(Y + (long long)(k * SR / 4 + w) * ys, (uint32_t)y[4 * w] | ((uint32_t)y[4 * w + 1] << 8) |
+                                                              ((uint32_t)y[4 * w + 2] << 16) | ((uint32_t)y[4 * w + 3] << 24));
         } else {
-            uint32_t* yw = Y + (long long)((k * S) >> 2) * ys;
-            const int sh = ((k * S) & 3) * 8;
+            uint32_t* yw = Y + (long long)((k * SR) >> 2) * ys;
+            const int sh = ((k * SR) & 3) * 8;
             uint32_t ws = 0;
 #pragma unroll
-            for (int t = 0; t < S; ++t) ws |= (uint32_t)y[t] << (8 * t);
+            for (int t = 0; t < SR; ++t) ws |= (uint32_t)y[t] << (8 * t);
             sty<YL>(yw, (sh == 0 ? 0u : (ldy<YL>(yw) & ((1u << sh) - 1u))) | (ws << sh));
         }
         // combine completed plus children: [(ym+yp)%q | (q-yp)%q]

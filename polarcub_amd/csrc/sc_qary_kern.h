@@ -24,9 +24,12 @@ constexpr int qary_waves(int q, int S, int G = 4) {
 }
 
 // YL: the re-encoded symbols in dynamic LDS ([Nv/4 words][kQaryBlock]) instead of the slot
-template <int Q, int S, int G, int W = qary_waves(Q, S, G), int U = 1, bool YL = false>
+// HL: the split last level's LDS half after them ([S * Q doubles][kQaryBlock], decode_qary_cw)
+template <int Q, int S, int G, int W = qary_waves(Q, S, G), int U = 1, bool YL = false, bool HL = false>
 __global__ __launch_bounds__(kQaryBlock, W) void k_sc_qary(QArgs A) {
+    static_assert(kQaryBlock == kQHlStride, "split-level LDS column stride");
     extern __shared__ uint32_t qsym_lds[];
+    double* hl = HL ? (double*)(qsym_lds + A.ylds_words * kQaryBlock) + threadIdx.x : nullptr;
     constexpr int CWB = kQaryBlock / G;  // codewords per tile
     const long long slot = (long long)blockIdx.x * kQaryBlock + threadIdx.x;
     const int j = threadIdx.x & (G - 1);
@@ -35,8 +38,8 @@ __global__ __launch_bounds__(kQaryBlock, W) void k_sc_qary(QArgs A) {
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_qary_cw<Q, S, G, U, YL>(A, valid ? cw : A.B - 1, slot, valid, j, lane,
-                                       YL ? qsym_lds + threadIdx.x : nullptr, kQaryBlock);
+        decode_qary_cw<Q, S, G, U, YL, HL>(A, valid ? cw : A.B - 1, slot, valid, j, lane,
+                                           YL ? qsym_lds + threadIdx.x : nullptr, kQaryBlock, hl);
     }
 }
 
@@ -51,6 +54,9 @@ QKern qary_kernel_q78(int q, int S, int G);
 
 // the symbols-in-LDS twin of the kernel for (q, S, G), or nullptr (q = 4, S = 4, G = 4 only)
 QKern qary_kernel_q4_y(int S, int G);
+// its split-level twin (2S positions per lane at the chain's end, S of them in LDS; three waves)
+QKern qary_kernel_q4_h(int S, int G);
+inline QKern qary_kernel_h(int q, int S, int G) { return q == 4 ? qary_kernel_q4_h(S, G) : nullptr; }
 inline QKern qary_kernel_y(int q, int S, int G) { return q == 4 ? qary_kernel_q4_y(S, G) : nullptr; }
 
 inline QKern qary_kernel(int q, int S, int G) {

@@ -25,4 +25,11 @@ QKern qary_kernel_q4_y(int S, int G) {
     return nullptr;
 }
 
+// the split-level twin: 2S = 8 positions per lane at a chain's end, 4 of them in LDS (48 KB a
+// workgroup with the symbols, three workgroups a CU)
+QKern qary_kernel_q4_h(int S, int G) {
+    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 3, 1, true, true>;
+    return nullptr;
+}
+
 }  // namespace pcub

@@ -140,6 +140,16 @@ def set_qary_lanes(g):
     return old
 
 
+def set_qary_hl(on):
+    """Split last level of the q-ary decode kernel (2S positions per lane at a chain's end, S of
+    them in LDS: one stored stage depth fewer) where it exists and fits (True, the default) or
+    not (False).  Returns the previous setting."""
+    old = int(_lib.lib().pcub_sc_set_qary_hl(1 if on else 0))
+    if old < 0:
+        raise ValueError("pcub_sc_set_qary_hl")
+    return bool(old)
+
+
 def set_qary_lds(on):
     """Re-encoded symbols of the q-ary decode kernel in LDS where a kernel for it exists and
     fits (True, the default) or in the per-slot workspace (False).  Returns the previous setting."""

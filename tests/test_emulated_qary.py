@@ -36,8 +36,9 @@ def run(xy, frozen, q, S):
     return info[:K].T, xh.T
 
 
-@pytest.mark.parametrize("S", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("S", [1, 2, 4, 8, 16, -1, -2, -4, -8])
 def test_qsc_golden(S):
+    """S < 0: the split-level schedule (HL) with |S| register positions."""
     g = load_golden("qsc_q4_n256")
     info, _ = run(g["table"][g["y"]], g["frozen"], 4, S)
     assert np.array_equal(info, g["info"])
@@ -54,8 +55,8 @@ def test_random_vs_oracle(q):
         xy = rng.random((B, N, q))
         xy[rng.random((B, N)) < 0.05] = 0.0
         ri, rx = orc.decode_qary(q, xy, frozen)
-        for S in (1, 2, 4, 8, 16):
-            if N < 2 * S:
+        for S in (1, 2, 4, 8, 16, -1, -2, -4):
+            if N < (-4 * S if S < 0 else 2 * S):
                 continue
             info, xh = run(xy, frozen, q, S)
             assert np.array_equal(info, ri), (q, N, S)

@@ -18,11 +18,13 @@ def lanes(request):
     sc.set_qary_lanes(old)
 
 
-@pytest.mark.parametrize("lds", [True, False])
-def test_qsc_q4_n256_matches_reference(lanes, lds):
-    """lds: the re-encoded symbols in LDS (the C4 kernel's default) or in the workspace."""
+@pytest.mark.parametrize("lds,hl", [(True, True), (True, False), (False, False)])
+def test_qsc_q4_n256_matches_reference(lanes, lds, hl):
+    """lds: the re-encoded symbols in LDS (the C4 kernel's default) or in the workspace; hl: the
+    split last level (default with the symbols in LDS at G = 4) or not."""
     from polarcub_amd import sc
     old_lds = sc.set_qary_lds(lds)
+    old_hl = sc.set_qary_hl(hl)
     g = load_golden("qsc_q4_n256")
     code = sc.QaryCode(4, 256, g["frozen"])
     dec = sc.QaryDecoder(code)
@@ -34,6 +36,7 @@ def test_qsc_q4_n256_matches_reference(lanes, lds):
     enc = sc.encode_qary(code, info)
     assert torch.equal(enc, xhat)
     sc.set_qary_lds(old_lds)
+    sc.set_qary_hl(old_hl)
 
 
 def test_qary_q3_matches_reference(lanes):

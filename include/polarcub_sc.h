@@ -191,6 +191,15 @@ int pcub_sc_prior_bin(const double* xy, const double* px, int64_t px_batch, int6
  * m = p / s, (0.5, 0.5) when s = 0.  count values in, [count][2] f64 out. */
 int pcub_leaf_marginals(const double* leaf, int64_t count, double* marginals, void* stream);
 
+/* Binary SC decode of compact normalised rows: xc [N][B] f64, +r standing for the joint row
+ * (1, r) and -r for (r, 1) (NaN: (0, 0)).  The same decode as pcub_sc_decode_bin on those pairs
+ * (the reference's arithmetic on a row with a 1 in it is the compact one), from 8 bytes a position
+ * instead of 16.  Workspace: pcub_sc_decode_bin_compact_workspace(B, log2N) bytes. */
+size_t pcub_sc_decode_bin_compact_workspace(int64_t B, int32_t log2N);
+int pcub_sc_decode_bin_compact(const double* xc, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                               const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
+                               uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Device Monte-Carlo (encodeDecodeSimulation, BinaryPolarEncoderDecoder.py:328-387, as a
  * batched pipeline).  Codeword g's draws come from Philox4x32-10 keyed by (seed, g), so
  * the codewords [offset, offset + B) are identical whichever rank or chunk makes them.
@@ -198,13 +207,17 @@ int pcub_leaf_marginals(const double* leaf, int64_t count, double* marginals, vo
  *   pcub_mc_channel  codeword bits [ceil(N/32)][B] -> joint pairs [N][B][2] f64;
  *                    channel 0 = BI-AWGN (param = sigma^2, BPSK 0 -> +1),
  *                    channel 1 = BSC (param = p, makeBSC's table)
+ *   pcub_mc_channel_norm  the same draws as normalised rows (each divided by its larger entry:
+ *                    the same channel law), compact ([N][B] f64, compact != 0) or as pairs
  *   pcub_mc_count_errors  counters[0] += B, [1] += frame errors, [2] += bit errors
- *   pcub_mc_run_bin  info -> encode -> channel -> decode -> count for codewords
+ *   pcub_mc_run_bin  info -> encode -> channel (normalised, compact) -> decode -> count for codewords
  *                    [offset, offset + count), chunk codewords at a time; counters
  *                    (device u64[4]) accumulate; the caller zeroes them. */
 int pcub_mc_info(uint64_t seed, int64_t offset, int64_t B, int32_t K, uint32_t* info_words, void* stream);
 int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel, double param,
                     const uint32_t* x_words, double* xy, void* stream);
+int pcub_mc_channel_norm(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel, double param,
+                         const uint32_t* x_words, double* out, int32_t compact, void* stream);
 int pcub_mc_count_errors(const uint32_t* decoded_words, const uint32_t* sent_words, int64_t B, int32_t K,
                          uint64_t* counters, void* stream);
 size_t pcub_mc_run_bin_workspace(int64_t chunk, int32_t log2N, int32_t K);

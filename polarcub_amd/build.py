@@ -28,7 +28,7 @@ ARCH = os.environ.get("PCUB_ARCH", "gfx950")
 
 SOURCES = ["sc_del_n4.hip", "sc_del_n4o.hip", "sc_del_n4x.hip", "sc_del_n3.hip", "sc_del_n3o.hip", "sc_del_n3x.hip",
            "sc_del_n2.hip", "sc_del_n2o.hip", "sc_del_n2x.hip", "sc_del_n1.hip", "sc_del_n1o.hip", "sc_del_n1x.hip",
-           "sc_bin.hip", "sc_bin_k0.hip", "sc_bin_k1.hip", "sc_bin_k2.hip", "sc_bin_k3.hip", "sc_bin_k4.hip", "sc_bin_k5.hip", "sc_qary.hip",
+           "sc_bin.hip", "sc_bin_k0.hip", "sc_bin_k1.hip", "sc_bin_k2.hip", "sc_bin_k3.hip", "sc_bin_k4.hip", "sc_bin_k5.hip", "sc_bin_k6.hip", "sc_qary.hip",
            "sc_qary_q2.hip", "sc_qary_q3.hip", "sc_qary_q4.hip", "sc_qary_q56.hip", "sc_qary_q78.hip",
            "sc_util.hip", "sc_del.hip", "sc_leaf.hip", "sc_qary_log.hip", "scl.hip",
            "sc_mc.hip"]
@@ -139,6 +139,9 @@ def up_to_date():
 
 def _compile(src, verbose):
     obj = _obj(src)
+    # the stamp records the sources as they were when the compile started: a header edited while
+    # the compiler runs leaves the object stale for the next build instead of wrongly current
+    dig = _obj_digest(src)
     tmp = obj + ".tmp.o"
     cmd = [HIPCC] + CFLAGS + ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-c", os.path.join(CSRC, src),
                               "-o", tmp]
@@ -146,10 +149,18 @@ def _compile(src, verbose):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, obj)
-    _write_stamp(obj, _obj_digest(src))
+    _write_stamp(obj, dig)
 
 
 def build(force=False, verbose=False):
+    import fcntl
+    os.makedirs(LIBDIR, exist_ok=True)
+    with open(os.path.join(LIBDIR, ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)  # one build at a time in this tree
+        return _build_locked(force, verbose)
+
+
+def _build_locked(force, verbose):
     build_host(force, verbose)
     if not force and up_to_date():
         return LIB
@@ -157,13 +168,14 @@ def build(force=False, verbose=False):
     todo = [s for s in SOURCES if force or _stale(_obj(s), _obj_digest(s))]
     with ThreadPoolExecutor(max(1, min(len(todo), int(os.environ.get("MAX_JOBS", "8"))))) as ex:
         list(ex.map(lambda s: _compile(s, verbose), todo))
+    lib_dig = _lib_digest()
     tmp = LIB + ".tmp"
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC"] + [_obj(s) for s in SOURCES] + ["-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
-    _write_stamp(LIB, _lib_digest())
+    _write_stamp(LIB, lib_dig)
     return LIB
 
 

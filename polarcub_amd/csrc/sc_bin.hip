@@ -176,15 +176,19 @@ extern "C" size_t pcub_sc_decode_bin_workspace(int64_t B, int32_t log2N) {
     return ef_bytes(log2N, v) + (size_t)g * kBlock * slot_bytes(log2N, v);
 }
 
-extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
-                                  const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
-                                  uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream) {
+namespace {
+
+// raw pairs xy, or compact rows xc through a variant's compact-root twin (the caller checks one exists)
+int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                    const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
+                    uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream) {
     if (B < 0 || log2N < 0 || log2N > 24 || !frozen_mask || !frozen_val) return PCUB_EINVAL;
-    if (K < 0 || K > (1 << log2N) || (K > 0 && !info_words) || (B > 0 && !xy)) return PCUB_EINVAL;
+    if (K < 0 || K > (1 << log2N) || (K > 0 && !info_words) || (B > 0 && !xy && !xc)) return PCUB_EINVAL;
     if (B == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     BinArgs A;
     A.xy = (const double2*)xy;
+    A.xc = xc;
     A.B = B;
     A.n = log2N;
     A.fmask = frozen_mask;
@@ -227,6 +231,64 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
     A.nslots = nslots;
     A.scratch = (double2*)slots;
     A.ybits = kVar[v].Y ? nullptr : (uint32_t*)(slots + (size_t)nslots * (Nv / 2 - bin_sr(v)) * sizeof(double2));
-    hipLaunchKernelGGL(variant_kernel(v), dim3((unsigned)g), dim3(kBlock), launch_lds(v, log2N), st, A);
+    const BinKernFn kern = xc ? bin_kernel_compact(v) : variant_kernel(v);
+    if (!kern) return PCUB_EINVAL;
+    hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(kBlock), launch_lds(v, log2N), st, A);
     return (int)hipGetLastError();
+}
+
+// compact normalised rows -> (1, r) / (r, 1) pairs; NaN -> (0, 0)
+__global__ __launch_bounds__(kBlock) void k_expand_compact(const double* xc, long long count, double2* xy) {
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= count) return;
+    const double v = xc[i];
+    const double r = __builtin_fabs(v);
+    double2 o;
+    if (v != v) o = double2{0.0, 0.0};
+    else if (__builtin_signbit(v)) o = double2{r, 1.0};
+    else o = double2{1.0, r};
+    xy[i] = o;
+}
+
+// the compact path runs a compact-root kernel when the variant picked for 2^n has one (and the
+// code is past the small-code kernels); otherwise the rows are expanded into the workspace
+bool compact_direct(int n) { return n > 5 && bin_kernel_compact(pick_variant(n)) != nullptr; }
+
+}  // namespace
+
+extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                                  const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
+                                  uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!xy && B > 0) return PCUB_EINVAL;
+    return decode_bin_impl(xy, nullptr, B, log2N, frozen_mask, frozen_val, K, info_words, xhat_words, u_words,
+                           workspace, workspace_bytes, stream);
+}
+
+extern "C" size_t pcub_sc_decode_bin_compact_workspace(int64_t B, int32_t log2N) {
+    if (B <= 0 || log2N < 0 || log2N > 24) return 0;
+    const size_t w = pcub_sc_decode_bin_workspace(B, log2N);
+    if (compact_direct(log2N)) return w;
+    return ((w + 255) & ~(size_t)255) + (size_t)B * ((size_t)1 << log2N) * sizeof(double2);
+}
+
+extern "C" int pcub_sc_decode_bin_compact(const double* xc, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                                          const uint32_t* frozen_val, int32_t K, uint32_t* info_words,
+                                          uint32_t* xhat_words, uint32_t* u_words, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+    if (B < 0 || log2N < 0 || log2N > 24) return PCUB_EINVAL;
+    if (B == 0) return 0;
+    if (!xc || !workspace) return PCUB_EINVAL;
+    if (compact_direct(log2N))
+        return decode_bin_impl(nullptr, xc, B, log2N, frozen_mask, frozen_val, K, info_words, xhat_words, u_words,
+                               workspace, workspace_bytes, stream);
+    const size_t w = pcub_sc_decode_bin_workspace(B, log2N);
+    const size_t off = (w + 255) & ~(size_t)255;
+    const long long count = B * (1LL << log2N);
+    if (workspace_bytes < off + (size_t)count * sizeof(double2)) return PCUB_EINVAL;
+    double2* xy = (double2*)((char*)workspace + off);
+    hipLaunchKernelGGL(k_expand_compact, dim3((unsigned)((count + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, xc, count, xy);
+    if (hipGetLastError() != hipSuccess) return (int)hipErrorLaunchFailure;
+    return decode_bin_impl((const double*)xy, nullptr, B, log2N, frozen_mask, frozen_val, K, info_words, xhat_words,
+                           u_words, workspace, w, stream);
 }

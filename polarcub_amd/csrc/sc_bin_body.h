@@ -34,6 +34,7 @@ namespace pcub {
 
 struct BinArgs {
     const double2* xy;         // [N][B] raw pairs
+    const double* xc;          // [N][B] compact normalised rows (the CR kernels' root instead of xy)
     long long B;
     int n;                     // log2 N
     const uint32_t* fmask;     // ceil(N/32)
@@ -204,6 +205,7 @@ struct Lvl {
 // the partial sums of the first op's minus child when that op is a plus transform.
 struct Chain {
     const double2* in;  // root: this lane's row 2*bitrev_{nv-1}(t) at in[2*bitrev(t)*B] (lane part folded in)
+    const double* inc;  // compact root (R == 3): the same rows, one double each
     long long B;
     int nv;             // log2 of the virtual (per-lane) length
     Lvl src;            // compact source level (depth a > 0)
@@ -222,6 +224,19 @@ typedef double d2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) d2v gd2v;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 #endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(1))) double gd1;
+#endif
+
+// one double of the compact root (non-temporal: streamed twice, far apart)
+PCUB_HD double ld1nt(const double* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_nontemporal_load((const gd1*)p);
+#else
+    return *p;
+#endif
+}
 
 template <bool NT = false, bool GL = true>
 PCUB_HD double2 ld2(const double2* p) {

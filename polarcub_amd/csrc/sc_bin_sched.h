@@ -21,10 +21,13 @@ namespace pcub {
 // bits) and a compute stage, so a pass can issue the loads of later columns before it
 // computes the current one (software pipelining: the HBM latency of a column is covered by
 // the arithmetic of the columns before it instead of by other waves alone).
+// R: 0 = a stored compact level, 1 / 2 = the raw root (plain / non-temporal loads), 3 = a
+// compact root (normalised rows, one double each: the root transforms are then the compact
+// ones, which is the reference's arithmetic on rows (1, r) / (r, 1) exactly).
 template <int F, bool FG, int R>
 struct ColLoad {
     static constexpr int H = 1 << (F - 1);
-    static constexpr int NX = R != 0 ? 4 * H : 2 * H;  // 16-byte values loaded
+    static constexpr int NX = (R == 1 || R == 2) ? 4 * H : 2 * H;  // 16-byte values loaded
     double2 x[NX];
     uint32_t w[FG ? H : 1];  // minus-child bits of column P at bit 0, P+1 at bit 1
 };
@@ -39,7 +42,13 @@ PCUB_HD void col_load(const Chain& c, int p, int C, ColLoad<F, FG, R>& L) {
             const int bp = c.ystart + P;  // even: bits bp, bp+1 share a word
             L.w[m] = ldy<YL>(c.Y + (long long)(bp >> 5) * c.ns) >> (bp & 31);
         }
-        if constexpr (R != 0) {
+        if constexpr (R == 3) {
+            // (a, b) of column P at x[2m], of column P+1 at x[2m+1]
+            const long long q0 = root_row(P, c.nv);
+            const long long q1 = q0 + (1LL << (c.nv - 2));
+            L.x[2 * m + 0] = double2{ld1nt(c.inc + (2 * q0) * c.B), ld1nt(c.inc + (2 * q0 + 1) * c.B)};
+            L.x[2 * m + 1] = double2{ld1nt(c.inc + (2 * q1) * c.B), ld1nt(c.inc + (2 * q1 + 1) * c.B)};
+        } else if constexpr (R != 0) {
             // positions P, P + Nv/2 are rows (2q, 2q+1); P+1 adds Nv/4 to q
             const long long q0 = root_row(P, c.nv);
             const long long q1 = q0 + (1LL << (c.nv - 2));
@@ -65,7 +74,11 @@ PCUB_HD void col_compute(const ColLoad<F, FG, R>& L, double2* y) {
             u1 = (L.w[m] >> 1) & 1u;
         }
         double2 o;
-        if constexpr (R != 0) {
+        if constexpr (R == 3) {
+            const double2 c0 = L.x[2 * m], c1 = L.x[2 * m + 1];
+            o.x = FG ? op_g(c0.x, c0.y, u0) : op_f(c0.x, c0.y);
+            o.y = FG ? op_g(c1.x, c1.y, u1) : op_f(c1.x, c1.y);
+        } else if constexpr (R != 0) {
             const double2 a0 = L.x[4 * m], b0 = L.x[4 * m + 1], a1 = L.x[4 * m + 2], b1 = L.x[4 * m + 3];
             o.x = FG ? op_g_raw(a0, b0, u0) : op_f_raw(a0, b0);
             o.y = FG ? op_g_raw(a1, b1, u1) : op_f_raw(a1, b1);
@@ -277,7 +290,7 @@ PCUB_HD uint64_t hl_frozen(uint64_t* ub, const uint64_t* fv, int j) {
 // HL: the chain ends at a split level of SR = 2S values per lane (first half in the LDS column
 //     hl, second half in registers; hl_run), one stored stage depth fewer than the plain S
 // PF: prefetch distance of the final passes (column pairs whose loads are in flight ahead)
-template <int S, int G, bool LDS = false, int NT = 0, bool YL = false, bool HL = false, int PF = 0>
+template <int S, int G, bool LDS = false, int NT = 0, bool YL = false, bool HL = false, int PF = 0, bool CR = false>
 PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
                              Lvl last = Lvl{nullptr, 0}, uint32_t* ylds = nullptr, long long ystride = 0,
                              double* hl = nullptr) {
@@ -291,7 +304,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     constexpr int SU = SR * G;  // real u positions per chain-end subtree (<= 256)
     using W = SubWin<SR, G>;   // window geometry (HL: the S-value halves run SubWin<S, G>)
     constexpr int NW = W::NW;
-    constexpr int RR = NT >= 1 ? 2 : 1;
+    constexpr int RR = CR ? 3 : NT >= 1 ? 2 : 1;  // root loads (CR: the compact root A.xc)
     constexpr bool NS = NT >= 2;
     const int n = A.n;
     const int nv = n - g;
@@ -299,7 +312,9 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     const int D = nv - s;
     const long long ns = A.nslots;
     const long long B = A.B;
-    const double2* in = A.xy + cw + 2 * (long long)bitrev((uint32_t)j, n - 1) * B;
+    const long long rowbase = cw + 2 * (long long)bitrev((uint32_t)j, n - 1) * B;
+    const double2* in = CR ? nullptr : A.xy + rowbase;
+    const double* inc = CR ? A.xc + rowbase : nullptr;
     double2* scr = A.scratch + slot;
     uint32_t* Y = YL ? ylds : A.ybits + slot;
     const long long ys = YL ? ystride : ns;  // Y word stride
@@ -320,7 +335,8 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     int infow = 0;
 
     for (int k = 0; k < (1 << D); ++k) {
-        in = launder(in);
+        if constexpr (CR) inc = launder(inc);
+        else in = launder(in);
         scr = launder(scr);
         if constexpr (!YL) Y = launder(Y);
         lm.scr = scr;
@@ -336,6 +352,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         bool fg = (k != 0);
         Chain c;
         c.in = in;
+        c.inc = inc;
         c.B = B;
         c.nv = nv;
         c.Y = Y;

@@ -140,6 +140,61 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_
     }
 }
 
+// Normalised channel rows (each joint row divided by its larger entry: the same channel law, and
+// no SC decision depends on a row's positive scale), as compact values (+r: (1, r), -r: (r, 1);
+// COMPACT, [N][B] doubles) or as the pairs they stand for ([N][B][2]).  BI-AWGN: the likelihood
+// ratio p0 / p1 = exp(2y / sigma^2), so the row is (1, exp(-2y/s2)) for y >= 0, else
+// (exp(2y/s2), 1); BSC: makeBSC's row normalised (norm_pack).  Same Philox draws as k_mc_channel.
+__device__ __forceinline__ double awgn_norm(const McArgs& A, uint32_t xb, double z) {
+    const double y = (xb ? -1.0 : 1.0) + A.sigma * z;
+    const double l = y * A.inv2s2 * 4.0;  // 2 y / sigma^2
+    const double r = exp(-__builtin_fabs(l));
+    return l >= 0.0 ? r : -r;
+}
+
+__device__ __forceinline__ double bsc_norm(const McArgs& A, uint32_t xb, double u) {
+    const double2 o = bsc_pair(A, xb, u);
+    return norm_pack(o.x, o.y);
+}
+
+__device__ __forceinline__ void put_norm(double* out, long long i, long long B, long long b, double c, bool compact) {
+    if (compact) {
+        out[i * B + b] = c;
+    } else {
+        const double r = __builtin_fabs(c);
+        ((double2*)out)[i * B + b] = __builtin_signbit(c) ? double2{r, 1.0} : double2{1.0, r};
+    }
+}
+
+template <bool COMPACT>
+__global__ __launch_bounds__(kMcBlock) void k_mc_channel_norm(McArgs A, const uint32_t* x, double* out) {
+    const long long b = (long long)blockIdx.x * kMcBlock + threadIdx.x;
+    if (b >= A.B) return;
+    const uint64_t g = (uint64_t)(A.offset + b);
+    const long long N = 1LL << A.n;
+    const long long pairs = (N + 1) / 2;
+    for (long long j = blockIdx.y; j < pairs; j += gridDim.y) {
+        const long long i0 = 2 * j;
+        const uint32_t xw = x[(i0 >> 5) * A.B + b] >> (i0 & 31);
+        const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)j, (uint32_t)A.seed,
+                            (uint32_t)(A.seed >> 32));
+        const double u0 = u01(r.v[0], r.v[1]), u1 = u01(r.v[2], r.v[3]);
+        double c0, c1;
+        if (A.channel == 0) {
+            const double rad = sqrt(-2.0 * log(u0));
+            double sn, cs;
+            sincos(6.283185307179586 * u1, &sn, &cs);
+            c0 = awgn_norm(A, xw & 1u, rad * cs);
+            c1 = awgn_norm(A, (xw >> 1) & 1u, rad * sn);
+        } else {
+            c0 = bsc_norm(A, xw & 1u, u0);
+            c1 = bsc_norm(A, (xw >> 1) & 1u, u1);
+        }
+        put_norm(out, i0, A.B, b, c0, COMPACT);
+        if (i0 + 1 < N) put_norm(out, i0 + 1, A.B, b, c1, COMPACT);
+    }
+}
+
 // counters[0] += B, [1] += frame errors, [2] += bit errors (information bits)
 __global__ __launch_bounds__(kMcBlock) void k_mc_count(const uint32_t* dec, const uint32_t* sent, long long B, int W,
                                                         unsigned long long* counters) {
@@ -271,6 +326,33 @@ extern "C" int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t
     return (int)hipGetLastError();
 }
 
+extern "C" int pcub_mc_channel_norm(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel,
+                                    double param, const uint32_t* x_words, double* out, int32_t compact, void* stream) {
+    if (B < 0 || offset < 0 || log2N < 0 || log2N > 24 || (channel != 0 && channel != 1)) return PCUB_EINVAL;
+    if (channel == 0 && !(param > 0.0)) return PCUB_EINVAL;
+    if (channel == 1 && !(param >= 0.0 && param <= 1.0)) return PCUB_EINVAL;
+    if (B == 0) return 0;
+    if (!x_words || !out) return PCUB_EINVAL;
+    McArgs A{seed, offset, B, log2N, 0, channel, param, 0.0, 0.0, 0.0};
+    if (channel == 0) {
+        A.sigma = sqrt(param);
+        A.inv2s2 = 1.0 / (2.0 * param);
+    }
+    const long long gx = (B + kMcBlock - 1) / kMcBlock;
+    const long long pairs = (((long long)1 << log2N) + 1) / 2;
+    long long gy = (16384 + gx - 1) / gx;
+    if (gy > pairs) gy = pairs;
+    if (gy > 65535) gy = 65535;
+    if (gx > 0x7fffffffLL) return PCUB_EINVAL;
+    if (compact)
+        hipLaunchKernelGGL(k_mc_channel_norm<true>, dim3((unsigned)gx, (unsigned)gy), dim3(kMcBlock), 0,
+                           (hipStream_t)stream, A, x_words, out);
+    else
+        hipLaunchKernelGGL(k_mc_channel_norm<false>, dim3((unsigned)gx, (unsigned)gy), dim3(kMcBlock), 0,
+                           (hipStream_t)stream, A, x_words, out);
+    return (int)hipGetLastError();
+}
+
 extern "C" int pcub_mc_info_qary(uint64_t seed, int64_t offset, int64_t B, int32_t K, int32_t q, uint8_t* info,
                                  void* stream) {
     if (B < 0 || offset < 0 || K < 0 || q < 2 || q > 255 || (K > 0 && B > 0 && !info)) return PCUB_EINVAL;
@@ -327,8 +409,8 @@ extern "C" int pcub_mc_count_errors(const uint32_t* decoded_words, const uint32_
 
 // ---------------------------------------------------------------------------
 // mc_run: the whole Monte-Carlo pipeline for codewords [offset, offset + count)
-// in chunks -- information bits -> polar encoder -> channel -> SC decode ->
-// error counters -- all stream-ordered on the device.
+// in chunks -- information bits -> polar encoder -> channel (normalised rows, compact) ->
+// SC decode (compact root) -> error counters -- all stream-ordered on the device.
 
 namespace {
 
@@ -348,7 +430,7 @@ McLayout mc_layout(int64_t chunk, int32_t log2N, int32_t K) {
     L.xy = L.x + align256(nw * chunk * 4);
     L.dec = L.xy + align256(N * chunk * 16);
     L.dws = L.dec + align256(iw * chunk * 4);
-    L.total = L.dws + align256(pcub_sc_decode_bin_workspace(chunk, log2N));
+    L.total = L.dws + align256(pcub_sc_decode_bin_compact_workspace(chunk, log2N));
     return L;
 }
 
@@ -375,9 +457,10 @@ extern "C" int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int
         int rc;
         if (K > 0 && (rc = pcub_mc_info(seed, offset + c0, B, K, info, stream))) return rc;
         if ((rc = pcub_polar_encode_bin(info, B, log2N, frozen_mask, frozen_val, K, x, stream))) return rc;
-        if ((rc = pcub_mc_channel(seed, offset + c0, B, log2N, channel, param, x, xy, stream))) return rc;
-        if ((rc = pcub_sc_decode_bin(xy, B, log2N, frozen_mask, frozen_val, K, dec, nullptr, nullptr, ws + L.dws,
-                                     L.total - L.dws, stream)))
+        // normalised rows in compact form (8 bytes a position) into the compact-root decode
+        if ((rc = pcub_mc_channel_norm(seed, offset + c0, B, log2N, channel, param, x, xy, 1, stream))) return rc;
+        if ((rc = pcub_sc_decode_bin_compact(xy, B, log2N, frozen_mask, frozen_val, K, dec, nullptr, nullptr,
+                                             ws + L.dws, L.total - L.dws, stream)))
             return rc;
         if ((rc = pcub_mc_count_errors(dec, info, B, K, counters, stream))) return rc;
     }

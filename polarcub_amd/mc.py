@@ -143,9 +143,27 @@ def philox_batch(code, seed, offset, B, channel, param):
     return info, xy
 
 
+def philox_norm_batch(code, seed, offset, B, channel, param, compact=True):
+    """Information words and the normalised channel rows of global codewords [offset, offset + B)
+    (the same draws as philox_batch, each row divided by its larger entry; pcub_mc_channel_norm):
+    compact [N, B] float64, or the pairs they stand for [N, B, 2]."""
+    from . import _lib
+    L = _lib.lib()
+    dev = code.device
+    info = torch.zeros((max(1, code.info_words), B), dtype=torch.int32, device=dev)
+    _lib.check(L.pcub_mc_info(int(seed), int(offset), B, code.K, sc._p(info), sc._stream()), "pcub_mc_info")
+    x = sc.encode_native(code, info)
+    shape = (code.N, B) if compact else (code.N, B, 2)
+    out = torch.empty(shape, dtype=torch.float64, device=dev)
+    _lib.check(L.pcub_mc_channel_norm(int(seed), int(offset), B, code.n, int(channel), float(param), sc._p(x),
+                                      sc._p(out), 1 if compact else 0, sc._stream()), "pcub_mc_channel_norm")
+    return info, out
+
+
 def run_bin(code, seed, offset, count, channel, param, chunk=1 << 18):
-    """encodeDecodeSimulation as one device pipeline (pcub_mc_run_bin) over global codewords
-    [offset, offset + count); returns [codewords, frame errors, bit errors, 0]."""
+    """encodeDecodeSimulation as one device pipeline (pcub_mc_run_bin: normalised channel rows in
+    compact form into the compact-root decode) over global codewords [offset, offset + count);
+    returns [codewords, frame errors, bit errors, 0]."""
     from . import _lib
     L = _lib.lib()
     chunk = int(max(1, min(chunk, count)))

@@ -215,6 +215,28 @@ class BinaryDecoder:
         _lib.check(rc, "pcub_sc_decode_bin")
         return info, xh, uo
 
+    def decode_compact_native(self, xc, want_xhat=True, out=None):
+        """xc: [N, B] float64 compact normalised rows on device (+r: (1, r), -r: (r, 1)), the same
+        decode as decode_native on those pairs (pcub_sc_decode_bin_compact).  Returns packed
+        (info_words, xhat_words | None, None)."""
+        c = self.code
+        if xc.dtype != torch.float64 or xc.dim() != 2 or xc.shape[0] != c.N or not xc.is_cuda:
+            raise ValueError("xc must be a float64 [N, B] device tensor with N=%d" % c.N)
+        xc = xc.contiguous()
+        B = xc.shape[1]
+        if out is None:
+            info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=xc.device)
+            xh = torch.empty((c.n_words, B), dtype=torch.int32, device=xc.device) if want_xhat else None
+        else:
+            info, xh, _ = out
+        need = int(_lib.lib().pcub_sc_decode_bin_compact_workspace(B, c.n))
+        if getattr(self, "_cws", None) is None or self._cws.numel() < need:
+            self._cws = torch.empty(max(need, 16), dtype=torch.uint8, device=xc.device)
+        rc = _lib.lib().pcub_sc_decode_bin_compact(_p(xc), B, c.n, _p(c.fmask_dev), _p(c.fval_dev), c.K, _p(info),
+                                                   _p(xh), None, _p(self._cws), self._cws.numel(), _stream())
+        _lib.check(rc, "pcub_sc_decode_bin_compact")
+        return info, xh, None
+
     def decode(self, xy):
         """xy: [B, N, 2] float64 (per-codeword rows, as the reference's probs).
         Returns (info [B, K] uint8, xhat [B, N] uint8)."""

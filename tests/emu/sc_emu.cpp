@@ -55,6 +55,43 @@ extern "C" int emu_decode_bin(const double* xy, long long B, int n, const uint32
     return 0;
 }
 
+// The compact-root schedule (CR: root rows as compact normalised doubles [N][B]).
+extern "C" int emu_decode_bin_compact(const double* xc, long long B, int n, const uint32_t* fmask,
+                                      const uint32_t* fval, uint32_t* info, uint32_t* xhat, int S, int hl) {
+    const int N = 1 << n;
+    const int SR = S;
+    if (n <= 5 || N < 2 * SR) return -1;
+    BinArgs A;
+    A.xy = nullptr;
+    A.xc = xc;
+    A.B = B;
+    A.n = n;
+    A.fmask = fmask;
+    A.fval = fval;
+    A.info = info;
+    A.xhat = xhat;
+    A.uout = nullptr;
+    const long long nslots = 4;
+    std::vector<double2> scr((size_t)(N / 2 - SR) * nslots + 1);
+    std::vector<uint32_t> yb((size_t)(N / 32 + 2) * nslots);
+    int s = 0;
+    while ((1 << s) < SR) ++s;
+    const int D = n - s;
+    std::vector<uint8_t> ef((size_t)1 << D);
+    for (int k = 0; k < (1 << D); ++k) ef[k] = (uint8_t)first_frozen_depth(fmask, k, D, SR);
+    A.ef = ef.data();
+    A.scratch = scr.data();
+    A.ybits = yb.data();
+    A.nslots = nslots;
+    (void)hl;  // the split level needs S*G >= 64 (not emulable at one lane per codeword)
+    for (long long b = 0; b < B; ++b) {
+        if (S == 8) decode_codeword<8, 1, false, 1, false, false, 0, true>(A, b, 0, 0, b % nslots, true);
+        else if (S == 16) decode_codeword<16, 1, false, 1, false, false, 0, true>(A, b, 0, 0, b % nslots, true);
+        else decode_codeword<32, 1, false, 1, false, false, 0, true>(A, b, 0, 0, b % nslots, true);
+    }
+    return 0;
+}
+
 // helper self-checks: polar_bits against the half-split recursion, gather_stride against a bit loop
 static uint64_t enc_rec(uint64_t u, int L) {
     if (L == 1) return u & 1u;

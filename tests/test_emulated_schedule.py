@@ -87,3 +87,38 @@ def test_schedule_rate0_blocks(n, S):
         ri, rx = orc.decode_bin(xy, frozen, fval)
         assert np.array_equal(info, ri) and np.array_equal(xhat, rx)
         assert np.all(u[:, frozen == 1] == fval[frozen == 1])
+
+
+@pytest.mark.parametrize("S", [8, 16, 32])
+@pytest.mark.parametrize("n", [6, 8, 10])
+def test_compact_root_schedule_matches_pairs(n, S):
+    """The compact-root schedule (CR: rows as compact normalised doubles) decodes exactly what the
+    pair schedule decodes on the pairs they stand for (zeros, -0.0, ties and a (0, 0) row in)."""
+    rng = np.random.default_rng(10 * n + S)
+    N, B = 1 << n, 40
+    if N < 2 * S:
+        pytest.skip("code shorter than two register subtrees")
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    frozen[: N // 8] = 1
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    r = rng.random((B, N)) ** 3
+    r[rng.random((B, N)) < 0.03] = 0.0
+    r[rng.random((B, N)) < 0.02] = 1.0
+    xc = np.where(rng.random((B, N)) < 0.5, r, -r)
+    xc[0, 1] = -0.0
+    xc[2, 3] = np.nan
+    ab = np.abs(xc)
+    pairs = np.where(np.signbit(xc)[..., None], np.stack([ab, np.ones_like(ab)], -1),
+                     np.stack([np.ones_like(ab), ab], -1))
+    pairs[2, 3] = 0.0
+    info_p, xh_p, _ = run(pairs, frozen, fval, S)
+    K = int(N - frozen.sum())
+    fm = pack_rows(frozen).reshape(-1).copy()
+    fv = pack_rows(fval).reshape(-1).copy()
+    xct = np.ascontiguousarray(xc.T)
+    info = np.zeros((max(1, (K + 31) // 32), B), np.uint32)
+    xh = np.zeros((max(1, (N + 31) // 32), B), np.uint32)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    assert emu().emu_decode_bin_compact(P(xct), ctypes.c_longlong(B), n, P(fm), P(fv), P(info), P(xh), S, 0) == 0
+    assert np.array_equal(unpack_rows(info, K), info_p)
+    assert np.array_equal(unpack_rows(xh, N), xh_p)

@@ -217,3 +217,68 @@ def test_deletion_sharded_counters_match_single_run(dcode):
     one = run(0, 2 * B)
     a, b = run(0, B), run(B, B)
     assert one == (a[0] + b[0], a[1] + b[1]) and one[0] > 0
+
+
+# -- compact normalised rows: the end-to-end pipeline's format ------------------------------------
+
+@pytest.mark.parametrize("n", [4, 6, 8, 10, 11, 12])
+def test_compact_decode_matches_pair_decode(n):
+    """pcub_sc_decode_bin_compact on compact rows = pcub_sc_decode_bin on the pairs they stand for
+    (compact-root kernels at N = 1024, 2048, 4096; expansion into the workspace elsewhere), zeros,
+    -0.0, ties (1.0) and a NaN (0, 0) row included."""
+    from polarcub_amd import sc
+    rng = np.random.default_rng(n)
+    N, B = 1 << n, 700
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    frozen[: N // 8] = 1
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    code = sc.CodeSpec(N, frozen, fval, device="cuda")
+    r = rng.random((N, B)) ** 3
+    r[rng.random((N, B)) < 0.02] = 0.0
+    r[rng.random((N, B)) < 0.01] = 1.0
+    xc = np.where(rng.random((N, B)) < 0.5, r, -r)
+    xc[0, 3] = -0.0
+    xc[5, 7] = np.nan
+    xct = torch.from_numpy(xc).cuda()
+    ab = np.abs(xc)
+    pairs = np.where(np.signbit(xc)[..., None], np.stack([ab, np.ones_like(ab)], -1), np.stack([np.ones_like(ab), ab], -1))
+    pairs[5, 7] = 0.0
+    dec = sc.BinaryDecoder(code)
+    i1, x1, _ = dec.decode_compact_native(xct)
+    i2, x2, _ = dec.decode_native(torch.from_numpy(pairs).cuda())
+    assert torch.equal(i1, i2) and torch.equal(x1, x2)
+
+
+def test_run_bin_matches_pair_pipeline(code):
+    """pcub_mc_run_bin (compact normalised rows -> compact-root decode) counts exactly what the
+    pair pipeline counts on the same normalised rows: info -> encode -> pcub_mc_channel_norm (pairs)
+    -> pcub_sc_decode_bin -> errors."""
+    from polarcub_amd import mc, sc
+    c, s2 = code
+    B = 5000
+    for ch, param in ((mc.CHANNEL_AWGN, s2), (mc.CHANNEL_BSC, 0.11)):
+        got = mc.run_bin(c, 44, 1000, B, ch, param, chunk=2048)
+        info, pairs = mc.philox_norm_batch(c, 44, 1000, B, ch, param, compact=False)
+        iw, _, _ = sc.BinaryDecoder(c).decode_native(pairs)
+        fe, be = mc.error_counts(sc.unpack(iw, c.K), sc.unpack(info, c.K))
+        assert got[:3] == [B, fe, be] and fe > 0
+        _, xc = mc.philox_norm_batch(c, 44, 1000, B, ch, param, compact=True)
+        ab = xc.abs()
+        assert torch.equal(torch.where(torch.signbit(xc), ab, torch.ones_like(ab)), pairs[..., 0])
+        assert torch.equal(torch.where(torch.signbit(xc), torch.ones_like(ab), ab), pairs[..., 1])
+
+
+def test_normalised_awgn_rows_follow_the_channel_law(code):
+    """The normalised BI-AWGN row of y is (1, exp(-2y/s2)) or (exp(2y/s2), 1): the implied
+    (1 - 2x) y ~ N(1, s2)."""
+    from polarcub_amd import mc
+    c, s2 = code
+    info, xc = mc.philox_norm_batch(c, 5, 0, 2048, mc.CHANNEL_AWGN, s2)
+    x = _x_bits(c, info)
+    v = xc.cpu().numpy()
+    y = np.where(np.signbit(v), 1.0, -1.0) * np.log(np.abs(v)) * s2 / 2.0
+    z = ((1.0 - 2.0 * x) * y - 1.0) / math.sqrt(s2)
+    fin = np.isfinite(z)
+    assert fin.mean() > 0.999
+    z = z[fin]
+    assert abs(z.mean()) < 5 / math.sqrt(z.size) and abs(z.var() - 1.0) < 5 * math.sqrt(2.0 / z.size)

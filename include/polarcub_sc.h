@@ -97,7 +97,7 @@ int pcub_polar_encode_bin(const uint32_t* info_words, int64_t B, int32_t log2N, 
  * Guardbands.py:47-93) builds from each received word.
  *   rx          [B][stride] u8 received symbols (0/1), rx_len[b] <= stride of them valid
  *   n, n0       code length 2^n, 2^n0 inputs per trellis; supported (decode):
- *               1 <= n0 <= 4, 1 <= n - n0 <= 8; leaf export: n - n0 <= 6 and ones = 0
+ *               1 <= n0 <= 4, 1 <= n - n0 <= 8 (decode and leaf export)
  *               (pcub_sc_deletion_supported / pcub_sc_leaf_deletion_supported)
  *   ones        numberOfOnesToAddAtBothEndsOfGuardbands, 0 <= ones <= 3
  *   pd          deletion probability the trellises are built with
@@ -126,6 +126,26 @@ int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, i
                           int32_t ones, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
                           const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
                           double* leaf, void* stream);
+
+/* n0 = 3 segment-state table (trellis depth 3, ones = 0): every value a trellis lane hands to
+ * the memoryless subtree is a function of its segment (m <= 8 received bits) and of the bits
+ * the subtree returned before it, so one 1 MiB table per pd replaces the per-lane trellis
+ * levels.  pcub_sc_deletion_table_bytes(n0) is its size (0: no table for n0);
+ * pcub_sc_deletion_build_table fills it on the stream (8-byte aligned device memory).
+ * The _tab twins of the two deletion entry points read it when n0 = 3 and ones = 0 and the
+ * table was built for the same pd (its stamp); otherwise, or with table = NULL, they decode
+ * as the plain entry points.  Decisions are identical either way. */
+int64_t pcub_sc_deletion_table_bytes(int32_t n0);
+int pcub_sc_deletion_build_table(int32_t n0, double pd, double* table, void* stream);
+int pcub_sc_decode_deletion_tab(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n,
+                                int32_t n0, int32_t ones, double pd, const uint32_t* frozen_mask,
+                                const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
+                                const double* table, void* stream);
+int pcub_sc_leaf_deletion_tab(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n,
+                              int32_t n0, int32_t ones, double pd, const uint32_t* frozen_mask,
+                              const uint32_t* frozen_val, const uint32_t* frozen_val_cw, int32_t K,
+                              uint32_t* info_words, uint32_t* xhat_words, double* leaf, const double* table,
+                              void* stream);
 /* q-ary SC in the log domain (QaryPolarEncoderDecoder(..., use_log=True).decode,
  * QaryPolarEncoderDecoder.py:318-401 over VectorDistributions/QaryMemorylessVectorDistribution.py
  * with use_log): logaddexp minus transform, logsumexp normalisation and marginal.

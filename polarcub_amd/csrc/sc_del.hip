@@ -19,6 +19,21 @@ namespace {
 
 constexpr int kMaxOnes = 3;
 
+// the n0 = 3 segment-state table: one thread per entry, 512 x 256 doubles (entry j of a row: value
+// k = floor(log2(j + 1)) after history j + 1 - 2^k; entry 255: pd)
+__global__ __launch_bounds__(256) void k_del_n03_table(double pd, double* tab) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= kN03States * kN03Row) return;
+    const int st = i / kN03Row, j = i % kN03Row;
+    if (j == kN03Row - 1) {
+        tab[i] = pd;
+        return;
+    }
+    int k = 0;
+    while ((2 << k) <= j + 1) ++k;
+    tab[i] = n03_table_entry(st, k, (uint32_t)(j + 1 - (1 << k)), pd);
+}
+
 DelKern del_kernel(int n0, int tb, bool exp, int ones) {
     if (ones < 0 || ones > kMaxOnes) return nullptr;
     const int oc = ones > 0 ? kMaxOnes : 0;
@@ -52,7 +67,7 @@ OnesProbs ones_probs(int ones, double pd) {
 int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n, int32_t n0,
                int32_t ones, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
                const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words, double* leaf,
-               void* stream) {
+               const double* table, void* stream) {
     const DelKern kern = del_kernel(n0, n - n0, exp, ones);
     if (!kern || B < 0 || stride < 0 || stride > 32767 || !frozen_mask || (!frozen_val && !frozen_val_cw))
         return PCUB_EINVAL;
@@ -74,6 +89,7 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     A.info = info_words;
     A.xhat = xhat_words;
     A.leaf = leaf;
+    A.tab3 = (n0 == 3 && ones == 0) ? table : nullptr;
     const long long cpb = kDelBlock >> (n - n0);
     long long grid = (B + cpb - 1) / cpb;
     // bit-packed received words in LDS when the group's words fit in 32 KiB (always for
@@ -114,7 +130,16 @@ extern "C" int pcub_sc_decode_deletion(const uint8_t* rx, const int32_t* rx_len,
                                        uint32_t* xhat_words, void* stream) {
     if (!frozen_val) return PCUB_EINVAL;
     return launch_del(false, rx, rx_len, B, stride, n, n0, ones, pd, frozen_mask, frozen_val, nullptr, K, info_words,
-                      xhat_words, nullptr, stream);
+                      xhat_words, nullptr, nullptr, stream);
+}
+
+extern "C" int pcub_sc_decode_deletion_tab(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride,
+                                           int32_t n, int32_t n0, int32_t ones, double pd, const uint32_t* frozen_mask,
+                                           const uint32_t* frozen_val, int32_t K, uint32_t* info_words,
+                                           uint32_t* xhat_words, const double* table, void* stream) {
+    if (!frozen_val) return PCUB_EINVAL;
+    return launch_del(false, rx, rx_len, B, stride, n, n0, ones, pd, frozen_mask, frozen_val, nullptr, K, info_words,
+                      xhat_words, nullptr, table, stream);
 }
 
 extern "C" int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n,
@@ -122,5 +147,25 @@ extern "C" int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, i
                                      const uint32_t* frozen_val, const uint32_t* frozen_val_cw, int32_t K,
                                      uint32_t* info_words, uint32_t* xhat_words, double* leaf, void* stream) {
     return launch_del(true, rx, rx_len, B, stride, n, n0, ones, pd, frozen_mask, frozen_val, frozen_val_cw, K,
-                      info_words, xhat_words, leaf, stream);
+                      info_words, xhat_words, leaf, nullptr, stream);
+}
+
+extern "C" int pcub_sc_leaf_deletion_tab(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride,
+                                         int32_t n, int32_t n0, int32_t ones, double pd, const uint32_t* frozen_mask,
+                                         const uint32_t* frozen_val, const uint32_t* frozen_val_cw, int32_t K,
+                                         uint32_t* info_words, uint32_t* xhat_words, double* leaf, const double* table,
+                                         void* stream) {
+    return launch_del(true, rx, rx_len, B, stride, n, n0, ones, pd, frozen_mask, frozen_val, frozen_val_cw, K,
+                      info_words, xhat_words, leaf, table, stream);
+}
+
+extern "C" int64_t pcub_sc_deletion_table_bytes(int32_t n0) {
+    return n0 == 3 ? (int64_t)kN03States * kN03Row * (int64_t)sizeof(double) : 0;
+}
+
+extern "C" int pcub_sc_deletion_build_table(int32_t n0, double pd, double* table, void* stream) {
+    if (n0 != 3 || !table || ((uintptr_t)table & 7u) || !(pd >= 0.0 && pd <= 1.0)) return PCUB_EINVAL;
+    hipLaunchKernelGGL(k_del_n03_table, dim3(kN03States * kN03Row / 256), dim3(256), 0, (hipStream_t)stream, pd,
+                       table);
+    return (int)hipGetLastError();
 }

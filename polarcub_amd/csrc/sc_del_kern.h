@@ -59,6 +59,7 @@ struct DelArgs {
     const uint32_t* fval_cw;  // [ceil(N/32)][B] per-codeword frozen values (export mode), or null
     double* leaf;           // [N][B] compact normalised leaves (export mode)
     int rw;                 // > 0: words per codeword of the bit-packed received words in LDS
+    const double* tab3;     // n0 = 3 without ones: the segment-state table (n03_table_entry), or null
 };
 
 // XSub (sc_bin_body.h) for the export mode: no rate-0 node is skipped and the two
@@ -350,7 +351,7 @@ struct DelCtx {
 // row of the memoryless node: without guard-band ones by trellis_collapse (no child
 // built), with ones by building the length-1 child and taking its marginal.
 template <int L, int OC, class PT>
-__device__ __forceinline__ void del_collapse(const PT& t, const uint32_t* dec, int ones, double& m0, double& m1) {
+PCUB_HD void del_collapse(const PT& t, const uint32_t* dec, int ones, double& m0, double& m1) {
     if constexpr (OC > 0) {
         if (ones > 0) {
             using Cap = DelCap<L, OC>;
@@ -421,6 +422,102 @@ struct DelBase {
         return x;
     }
 };
+
+// n0 = 3 without guard-band ones: as for n0 = 2 (trellis_n02.h), every value a lane hands to the
+// memoryless subtree is a function of its segment (m <= 8 received bits y, pd) and of the bits
+// the subtree returned before it: the k-th of the walk's 8 values (k = 0..7) depends on the k
+// earlier bits, so a segment state holds 1 + 2 + .. + 128 = 255 values, and there are 512 states
+// (2^m - 1 + y for m <= 8, and "no edges" for m > 8).  The table (1 MB, global memory: built once
+// per pd by pcub_sc_deletion_table, reused by every decode) replays DelBase / DelNode's walk with
+// the same functions in the same order, so its entries are the per-lane values bit for bit.
+constexpr int kN03States = 512;
+constexpr int kN03Row = 256;  // 255 values per state, then pd (the stamp the kernel checks)
+
+PCUB_HD int n03_state(int m, uint32_t y) { return (m >= 0 && m <= 8) ? (1 << m) - 1 + (int)y : kN03States - 1; }
+
+// value k (history hist: the k bits returned before it, bit i = the i-th) of state st
+PCUB_HD double n03_table_entry(int st, int k, uint32_t hist, double pd) {
+    constexpr int L = 8;
+    using Cap = DelCap<L, 0>;
+    BaseT<L> b;
+    if (st == kN03States - 1) {
+        b.m = L + 1;
+        b.y = 0;
+    } else {
+        int m = 0;
+        while ((2 << m) <= st + 1) ++m;
+        b.m = m;
+        b.y = (uint32_t)(st + 1 - (1 << m));
+    }
+    b.d = L - b.m;
+    b.pins = 0.5 * (1.0 - pd);
+    b.pdel = 0.5 * pd;
+    Trel<4, Cap::V, Cap::E(1)> c1;
+    Trel<2, Cap::V, Cap::E(2)> c2;
+    int idx = 0;
+    uint32_t y1[2] = {0u, 0u};
+    for (int half = 0; half < 2; ++half) {  // DelBase: the depth-1 minus child, then the plus child
+        trellis_transform_base<L>(b, c1, half ? &y1[0] : nullptr);
+        trellis_normalize<4>(c1);
+        uint32_t y2[2] = {0u, 0u};
+        for (int h2 = 0; h2 < 2; ++h2) {  // DelNode<8, T, 4>: its depth-2 children
+            trellis_transform<4>(c1, c2, h2 ? &y2[0] : nullptr);
+            trellis_normalize<2>(c2);
+            double m0, m1;  // DelNode<8, T, 2>: the two collapses
+            del_collapse<L, 0>(c2, nullptr, 0, m0, m1);
+            if (idx == k) return norm_pack(m0, m1);
+            const uint32_t xm = (hist >> idx++) & 1u;
+            del_collapse<L, 0>(c2, &xm, 0, m0, m1);
+            if (idx == k) return norm_pack(m0, m1);
+            const uint32_t xp = (hist >> idx++) & 1u;
+            y2[h2] = (xm ^ xp) | (xp << 1);
+        }
+        uint32_t x = 0;
+        for (int h = 0; h < 2; ++h)
+            x |= ((((y2[0] ^ y2[1]) >> h) & 1u) << (2 * h)) | (((y2[1] >> h) & 1u) << (2 * h + 1));
+        y1[half] = x;
+    }
+    return 0.0;  // not reached: k < 8
+}
+
+// DelBase's walk through the table: the 8 subtree inputs in order (both candidates for the next
+// one are loaded before the subtree call that picks between them, so the gather overlaps it),
+// then DelBase / DelNode's re-encoding of the 8 returned bits
+template <int T, bool EXP>
+__device__ __forceinline__ uint32_t del_n03_tab(const double* tb, DelCtx<T, EXP>& cx) {
+    uint32_t hist = 0;
+    double v = tb[0];
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k) {
+        double v0 = 0.0, v1 = 0.0;
+        if (k < 7) {
+            const uint32_t nx = (2u << k) - 1u + hist;
+            v0 = tb[nx];
+            v1 = tb[nx + (1u << k)];
+        }
+        const uint32_t b = cx.subtree(v) & 1u;
+        hist |= b << k;
+        v = b ? v1 : v0;
+    }
+    uint32_t w[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        uint32_t z[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t b0 = (hist >> (4 * i + 2 * j)) & 1u, b1 = (hist >> (4 * i + 2 * j + 1)) & 1u;
+            z[j] = (b0 ^ b1) | (b1 << 1);
+        }
+        uint32_t x = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) x |= ((((z[0] ^ z[1]) >> h) & 1u) << (2 * h)) | (((z[1] >> h) & 1u) << (2 * h + 1));
+        w[i] = x;
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) x |= ((((w[0] ^ w[1]) >> h) & 1u) << (2 * h)) | (((w[1] >> h) & 1u) << (2 * h + 1));
+    return x;
+}
 
 // n0 = 2: the two trellis levels on the register-resident representation
 // (trellis_n02.h); same recursion as DelNode.  Returns the 4-bit re-encoded slice.
@@ -542,6 +639,17 @@ __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint3
         if (m <= kN02L)
             for (int i = 0; i < m; ++i) y |= (uint32_t)(bit(s + i) & 1) << i;
         x = del_n02_tab(n02tab + n02_state(m, y) * kN02Row, cx);
+    } else if constexpr (N0 == 3 && OC == 0) {
+        // the segment-state table, when one was built for this pd (its stamp: entry 255 of state 0);
+        // a wave-uniform branch, the stamp is one scalar load
+        if (A.tab3 && __double_as_longlong(A.tab3[kN03Row - 1]) == __double_as_longlong(A.pd)) {
+            uint32_t y = 0;
+            if (m <= 8)
+                for (int i = 0; i < m; ++i) y |= (uint32_t)(bit(s + i) & 1) << i;
+            x = del_n03_tab(A.tab3 + (long long)n03_state(m, y) * kN03Row, cx);
+        } else {
+            x = DelBase<L, T, EXP>::run(base_segment<L>(bit, s, m, A.pd), cx);
+        }
     } else if constexpr (N0 >= 3 && OC == 0) {
         x = DelBase<L, T, EXP>::run(base_segment<L>(bit, s, m, A.pd), cx);
     } else {

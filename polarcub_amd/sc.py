@@ -605,15 +605,37 @@ def leaf_deletion_supported(n, n0, ones=0):
 class DeletionDecoder:
     """Batched SC decoder over the deletion channel (CollectionOfBinaryTrellises built from
     each received word with buildCollectionOfBinaryTrellises_uniformInput_deletion, with
-    `ones` guard-band ones) for one CodeSpec."""
+    `ones` guard-band ones) for one CodeSpec.  With use_table (the default) and n0 = 3, ones = 0
+    the decoder builds the segment-state table for pd once per device
+    (pcub_sc_deletion_build_table) and every decode reads it; decisions are identical without it."""
 
-    def __init__(self, code, n0, pd, ones=0):
+    def __init__(self, code, n0, pd, ones=0, use_table=True):
         self.code = code
         self.n0 = int(n0)
         self.pd = float(pd)
         self.ones = int(ones)
+        self.use_table = bool(use_table)
+        self._tables = {}
         if not deletion_supported(code.n, self.n0, self.ones):
             raise ValueError("no deletion kernel for n=%d, n0=%d, ones=%d" % (code.n, self.n0, self.ones))
+
+    def table(self, device):
+        """The segment-state table on `device` (a float64 device tensor), or None when the shape
+        has none or use_table is off."""
+        if not self.use_table or self.ones != 0:
+            return None
+        L = _lib.lib()
+        nbytes = int(L.pcub_sc_deletion_table_bytes(self.n0))
+        if nbytes == 0:
+            return None
+        key = str(device)
+        t = self._tables.get(key)
+        if t is None:
+            t = torch.empty(nbytes // 8, dtype=torch.float64, device=device)
+            _lib.check(L.pcub_sc_deletion_build_table(self.n0, self.pd, _p(t), _stream()),
+                       "pcub_sc_deletion_build_table")
+            self._tables[key] = t
+        return t
 
     def decode_native(self, rx, rx_len, want_xhat=True):
         """rx: [B, W] uint8 received symbols on device, rx_len: [B] int32.
@@ -628,9 +650,10 @@ class DeletionDecoder:
             raise ValueError("rx_len must have B entries")
         info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=rx.device)
         xh = torch.empty((c.n_words, B), dtype=torch.int32, device=rx.device) if want_xhat else None
-        rc = _lib.lib().pcub_sc_decode_deletion(_p(rx), _p(ln), B, W, c.n, self.n0, self.ones, self.pd,
-                                                _p(c.fmask_dev), _p(c.fval_dev), c.K, _p(info), _p(xh), _stream())
-        _lib.check(rc, "pcub_sc_decode_deletion")
+        rc = _lib.lib().pcub_sc_decode_deletion_tab(_p(rx), _p(ln), B, W, c.n, self.n0, self.ones, self.pd,
+                                                    _p(c.fmask_dev), _p(c.fval_dev), c.K, _p(info), _p(xh),
+                                                    _p(self.table(rx.device)), _stream())
+        _lib.check(rc, "pcub_sc_decode_deletion_tab")
         return info, xh
 
     def decode(self, rx, rx_len):
@@ -650,10 +673,10 @@ class DeletionDecoder:
         info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=rx.device)
         xh = torch.empty((c.n_words, B), dtype=torch.int32, device=rx.device)
         leaf = torch.empty((c.N, B), dtype=torch.float64, device=rx.device)
-        rc = _lib.lib().pcub_sc_leaf_deletion(_p(rx), _p(ln), B, W, c.n, self.n0, self.ones, self.pd,
-                                              _p(c.fmask_dev), _p(c.fval_dev), _p(fw), c.K, _p(info), _p(xh),
-                                              _p(leaf), _stream())
-        _lib.check(rc, "pcub_sc_leaf_deletion")
+        rc = _lib.lib().pcub_sc_leaf_deletion_tab(_p(rx), _p(ln), B, W, c.n, self.n0, self.ones, self.pd,
+                                                  _p(c.fmask_dev), _p(c.fval_dev), _p(fw), c.K, _p(info), _p(xh),
+                                                  _p(leaf), _p(self.table(rx.device)), _stream())
+        _lib.check(rc, "pcub_sc_leaf_deletion_tab")
         return unpack(info, c.K), unpack(xh, c.N), leaf_marginals(leaf)
 
 

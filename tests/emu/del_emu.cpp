@@ -12,6 +12,7 @@
 
 #include "trellis_body.h"
 #include "trellis_n02.h"
+#include "sc_del_kern.h"
 
 using namespace pcub;
 
@@ -57,6 +58,13 @@ template <int L>
 constexpr int depth_of(int len) {
     return (L / len == 1) ? 0 : (L / len == 2) ? 1 : (L / len == 4) ? 2 : (L / len == 8) ? 3 : 4;
 }
+
+// n0 = 3 without ones: every value handed to the memoryless subtree must equal its entry of the
+// kernel's segment-state table (sc_del_kern.h, n03_table_entry), indexed by the trellis's
+// segment and the bits the subtree returned to it before
+std::vector<int> g_k3;
+std::vector<uint32_t> g_h3;
+long long g_n03_checks = 0;
 
 // the kernel's top level for n0 >= 3 without ones: children of the implicit base trellis
 // (BaseT), which must equal the children of the stored one field by field
@@ -117,8 +125,27 @@ struct Node {
             Trel<1, Cap<L, OC>::V, Cap<L, OC>::E(depth_of<L>(1))> c;
             std::vector<double> vals(T);
             std::vector<int> xm;
+            auto check3 = [&](const std::vector<double>& v) {
+                if constexpr (L == 8 && OC == 0) {
+                    if (ones != 0 || g_k3.size() != T) return;
+                    for (size_t t = 0; t < T; ++t) {
+                        const int st = n03_state(g_base[t].m, g_base[t].y);
+                        const double e = n03_table_entry(st, g_k3[t], g_h3[t], g_base[t].pdel * 2.0);
+                        if (as_bits(e) != as_bits(v[t])) throw 7;
+                        ++g_n03_checks;
+                    }
+                }
+            };
+            auto record3 = [&](const std::vector<int>& bits) {
+                if (g_k3.size() != T) return;
+                for (size_t t = 0; t < T; ++t) g_h3[t] |= (uint32_t)(bits[t] & 1) << g_k3[t]++;
+            };
             for (int half = 0; half < 2; ++half) {
-                if (half) xm = mem_sc(vals, cx);
+                if (half) {
+                    check3(vals);
+                    xm = mem_sc(vals, cx);
+                    record3(xm);
+                }
                 for (size_t t = 0; t < T; ++t) {
                     const uint32_t d = half ? (uint32_t)xm[t] : 0u;
                     double c0, c1;
@@ -132,7 +159,9 @@ struct Node {
                     vals[t] = norm_pack(c0, c1);
                 }
                 if (half) {
+                    check3(vals);
                     const std::vector<int> xp = mem_sc(vals, cx);
+                    record3(xp);
                     for (size_t t = 0; t < T; ++t) out[t] = (uint32_t)((xm[t] ^ xp[t]) | (xp[t] << 1));
                 }
             }
@@ -252,6 +281,8 @@ void decode_one_oc(const uint8_t* w, int len, int n, double pd, int ones, Ctx& c
     const OnesProbs op = ones_probs(ones, pd);
     std::vector<Trel<L, Cap<L, OC>::V, Cap<L, OC>::E0>> base(T);
     g_base.assign(T, BaseT<16>{});
+    g_k3.assign(L == 8 ? T : 0, 0);
+    g_h3.assign(L == 8 ? T : 0, 0u);
     for (int t = 0; t < T; ++t) {
         int s, m;
         segment_of(bit, len, tb, t, s, m);
@@ -320,6 +351,7 @@ extern "C" int emu_decode_deletion(const uint8_t* rx, const int32_t* rx_len, lon
 }
 
 extern "C" void emu_set_n02(int on) { use_n02 = on != 0; }
+extern "C" long long emu_n03_checks() { return g_n03_checks; }
 
 // n0 >= 3 without ones: the top level from the implicit base trellis (checked against the stored one)
 extern "C" void emu_set_base(int on) { g_use_base = on != 0; }

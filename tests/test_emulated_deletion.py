@@ -155,10 +155,14 @@ def test_wide_shapes_vs_oracle(n0, n, ones, implicit_base):
         rx[i, :len(w)] = w
     L = emu()
     L.emu_base_checks.restype = ctypes.c_longlong
+    L.emu_n03_checks.restype = ctypes.c_longlong
     checks0 = L.emu_base_checks()
+    n03_0 = L.emu_n03_checks()
     info, xhat = run(rx, np.array([len(w) for w in words], np.int32), n, n0, pd, frozen, fval, ones)
     if implicit_base and n0 >= 3 and ones == 0:
         assert L.emu_base_checks() > checks0
+    if n0 == 3 and ones == 0:  # every n0 = 3 leaf value matched its segment-state table entry
+        assert L.emu_n03_checks() > n03_0
     for i, w in enumerate(words):
         xr, ir = tro.decode_deletion(w, n, n0, pd, frozen, fval, ones=ones)
         assert list(info[i]) == ir and list(xhat[i]) == xr, i

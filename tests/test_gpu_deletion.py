@@ -130,3 +130,35 @@ def test_facade_dispatch_and_mc_line():
             lambda r: deletion.buildCollectionOfBinaryTrellises_uniformInput_deletion(r, pd, xi, n, n0, 0),
             m["mc_trials"], frozen, commonRandomnessSeed=m["crs"], randomInformationSeed=m["info_seed"])
     assert buf.getvalue().strip().splitlines()[-1] == m["line"]
+
+
+@pytest.mark.parametrize("n", [5, 10, 11])
+def test_n03_table_paths_agree(sc, n):
+    """n0 = 3: the segment-state table (pcub_sc_deletion_build_table), the per-lane trellis
+    levels (no table) and a table built for another pd (its stamp does not match: the kernel
+    ignores it) decode identically, and agree with the oracle."""
+    n0, pd = 3, 0.1
+    N = 1 << n
+    rng = np.random.default_rng(31 + n)
+    prng = random.Random(n)
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    words = [tro.deletion_channel([int(b) for b in rng.integers(0, 2, N)], pd, prng) for _ in range(40)]
+    words += [[], [0] * 7, [1] * (N + 9)]
+    rxt, ln = sc.pad_words(words)
+    code = sc.CodeSpec(N, frozen, fval, device="cuda")
+    outs = []
+    for mode in ("table", "plain", "stale"):
+        d = sc.DeletionDecoder(code, n0, pd, use_table=(mode != "plain"))
+        if mode == "stale":
+            d._tables[str(rxt.device)] = sc.DeletionDecoder(code, n0, 0.2).table(rxt.device)
+        if mode == "table":
+            tab = d.table(rxt.device).cpu().numpy()
+            assert tab.shape == (512 * 256,) and np.all(tab[255::256] == pd)
+        info, xhat = d.decode(rxt, ln)
+        outs.append((info.cpu().numpy(), xhat.cpu().numpy()))
+    for o in outs[1:]:
+        assert np.array_equal(o[0], outs[0][0]) and np.array_equal(o[1], outs[0][1])
+    for i in list(range(0, len(words), 7)) + [len(words) - 1]:
+        x_ref, i_ref = tro.decode_deletion(words[i], n, n0, pd, frozen, fval)
+        assert list(outs[0][0][i]) == i_ref and list(outs[0][1][i]) == x_ref, i

@@ -8,9 +8,14 @@
 // (VectorDistributions/CollectionOfBinaryTrellises.py:106-129) from a received word.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
+#include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "polarcub_sc.h"
+#include "sc_del_dense.h"
 #include "sc_del_kern.h"
 
 using namespace pcub;
@@ -18,6 +23,39 @@ using namespace pcub;
 namespace {
 
 constexpr int kMaxOnes = 3;
+
+std::atomic<int> g_dense{1};  // the table-driven layout allowed (pcub_sc_set_deletion_dense)
+
+// n0 = 3 tables built by pcub_sc_deletion_build_table in this process, with their pd: the
+// table-driven kernel reads a table without checking its stamp, so it runs only on a (table, pd)
+// pair registered here; any other table goes to k_sc_del, which checks the stamp per launch.
+std::mutex g_tab_mu;
+std::vector<std::pair<const double*, uint64_t>> g_tabs;
+
+uint64_t pd_bits(double pd) {
+    uint64_t b;
+    std::memcpy(&b, &pd, sizeof b);
+    return b;
+}
+
+bool tab_registered(const double* t, double pd) {
+    if (!t) return false;
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    for (const auto& e : g_tabs)
+        if (e.first == t) return e.second == pd_bits(pd);
+    return false;
+}
+
+void tab_register(const double* t, double pd) {
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    for (auto& e : g_tabs)
+        if (e.first == t) {
+            e.second = pd_bits(pd);
+            return;
+        }
+    if (g_tabs.size() >= 64) g_tabs.erase(g_tabs.begin());  // bounded: the oldest falls back to k_sc_del
+    g_tabs.emplace_back(t, pd_bits(pd));
+}
 
 // the n0 = 3 segment-state table: one thread per entry, 512 x 256 doubles (entry j of a row: value
 // k = floor(log2(j + 1)) after history j + 1 - 2^k; entry 255: pd)
@@ -90,27 +128,38 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     A.xhat = xhat_words;
     A.leaf = leaf;
     A.tab3 = (n0 == 3 && ones == 0) ? table : nullptr;
-    const long long cpb = kDelBlock >> (n - n0);
+    DelKern k = kern;
+    long long cpb = kDelBlock >> (n - n0);
+    const long long rw = ((long long)stride + 31) / 32;
+    // the table-driven layout (sc_del_dense.h) when the stage has a table: n0 = 2 (built per
+    // workgroup) or n0 = 3 with the caller's table, no ones, 16 .. 256 trellises, and the
+    // group's received words fit LDS bit-packed
+    const bool dense = g_dense.load(std::memory_order_relaxed) && !exp && ones == 0 && (n0 == 2 || (n0 == 3 && tab_registered(A.tab3, pd))) && n - n0 >= 4 &&
+                       (long long)kDenseCPB * rw * 4 <= kDenseMaxRxLds && del_kernel_dense(n0, n - n0);
+    if (dense) {
+        k = del_kernel_dense(n0, n - n0);
+        cpb = kDenseCPB;
+    }
     long long grid = (B + cpb - 1) / cpb;
     // bit-packed received words in LDS when the group's words fit in 32 KiB (always for
     // the 64-trellis shapes; very long padded rows of small codes parse from HBM)
-    const long long rw = ((long long)stride + 31) / 32;
-    A.rw = (cpb * rw * 4 <= 32768) ? (int)rw : 0;
+    A.rw = (dense || cpb * rw * 4 <= 32768) ? (int)rw : 0;
     const size_t lds = A.rw ? (size_t)(cpb * rw * 4) : 0;
-    // n0 = 2 without ones: each workgroup first builds the segment-state table, so the launch
-    // is persistent (one resident grid striding over the codeword groups)
-    if (n0 == 2 && ones == 0) {
+    // n0 = 2 without ones (and the table-driven layout): each workgroup first builds the
+    // segment-state table, so the launch is persistent (one resident grid striding over the
+    // codeword groups)
+    if (dense || (n0 == 2 && ones == 0)) {
         int dev = 0, cus = 0, occ = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kDelBlock, lds) == hipSuccess && cus > 0 &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kDelBlock, lds) == hipSuccess && cus > 0 &&
             occ > 0) {
             const long long res = (long long)cus * occ;
             if (grid > res) grid = res;
         }
     }
     if (grid * kDelBlock > 0xffffffffLL) return PCUB_EINVAL;  // 32-bit dispatch grid (work-items)
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kDelBlock), lds, (hipStream_t)stream, A);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kDelBlock), lds, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
 
@@ -159,6 +208,10 @@ extern "C" int pcub_sc_leaf_deletion_tab(const uint8_t* rx, const int32_t* rx_le
                       info_words, xhat_words, leaf, table, stream);
 }
 
+extern "C" int pcub_sc_set_deletion_dense(int32_t on) {
+    return g_dense.exchange(on ? 1 : 0);
+}
+
 extern "C" int64_t pcub_sc_deletion_table_bytes(int32_t n0) {
     return n0 == 3 ? (int64_t)kN03States * kN03Row * (int64_t)sizeof(double) : 0;
 }
@@ -167,5 +220,7 @@ extern "C" int pcub_sc_deletion_build_table(int32_t n0, double pd, double* table
     if (n0 != 3 || !table || ((uintptr_t)table & 7u) || !(pd >= 0.0 && pd <= 1.0)) return PCUB_EINVAL;
     hipLaunchKernelGGL(k_del_n03_table, dim3(kN03States * kN03Row / 256), dim3(256), 0, (hipStream_t)stream, pd,
                        table);
-    return (int)hipGetLastError();
+    const int rc = (int)hipGetLastError();
+    if (rc == 0) tab_register(table, pd);
+    return rc;
 }

@@ -1,0 +1,227 @@
+// sc_del_dense.h -- the table-driven deletion decoder: n0 = 2 or 3, no guard-band ones,
+// 16 .. 256 trellises, decode mode.
+//
+// With a segment-state table (trellis_n02.h for n0 = 2, n03_table_entry for n0 = 3) a trellis
+// costs one table load per subtree input, so the trellis stages no longer need a lane each:
+// k_sc_del's layout (one lane per trellis, the memoryless subtree decoded by 16 lanes of wave 0
+// after an LDS exchange and two barriers) leaves three waves of four idle in every subtree call.
+// Here a codeword owns G = 16 lanes of one wave for the whole decode (four codewords a wave,
+// sixteen a workgroup): lane j holds the LV = T / 16 trellises at memoryless positions
+// p = j + 16 t, looks their values up, and decodes the subtree in registers with the binary
+// kernel's WinTree / DelWin.  No LDS exchange and no barrier inside the walk.
+//
+// Same decisions as k_sc_del (and the reference): the values are the table's, which are the
+// per-lane values bit for bit (tests/emu/del_emu.cpp checks every one), the subtree is the same
+// WinTree over the same 16-lane layout k_sc_del's wave 0 uses, and the segment parse is
+// segment_of's descent (Guardbands.py:47-93) shared between the lane's trellises.
+#pragma once
+
+#include "sc_del_kern.h"
+
+namespace pcub {
+
+constexpr int kDenseG = 16;                     // lanes per codeword
+constexpr int kDenseCPB = kDelBlock / kDenseG;  // codewords per workgroup
+constexpr int kDenseMaxRxLds = 48 * 1024;       // bit-packed received words per workgroup, at most
+
+// slot of subtree input k (history hist: bit i = the i-th returned bit) in a state's row
+template <int N0>
+PCUB_HD int dense_slot(int k, uint32_t hist) {
+    if constexpr (N0 == 3) {
+        return (1 << k) - 1 + (int)hist;
+    } else {  // trellis_n02.h's order: [0] v1, [1 + xm] v2, [3 + ym] v3, [7 + 2 ym + xm'] v4
+        const uint32_t h0 = hist & 1u, h1 = (hist >> 1) & 1u, ym = (h0 ^ h1) | (h1 << 1);
+        return k == 0 ? 0 : k == 1 ? 1 + (int)h0 : k == 2 ? 3 + (int)ym : 7 + 2 * (int)ym + (int)((hist >> 2) & 1u);
+    }
+}
+
+// the re-encoding DelNode / DelBase apply to a trellis's returned bits: x[2h] = ym[h] ^ yp[h],
+// x[2h+1] = yp[h] over the two halves, recursively
+template <int L>
+PCUB_HD uint32_t enc_hist(uint32_t h) {
+    if constexpr (L == 1) {
+        return h & 1u;
+    } else {
+        constexpr int H = L / 2;
+        const uint32_t ym = enc_hist<H>(h), yp = enc_hist<H>(h >> H);
+        uint32_t x = 0;
+#pragma unroll
+        for (int i = 0; i < H; ++i) x |= ((((ym ^ yp) >> i) & 1u) << (2 * i)) | (((yp >> i) & 1u) << (2 * i + 1));
+        return x;
+    }
+}
+
+constexpr int cbitrev(int x, int nbits) {
+    int r = 0;
+    for (int i = 0; i < nbits; ++i) r |= ((x >> i) & 1) << (nbits - 1 - i);
+    return r;
+}
+
+// bits [s, s + m) of a bit-packed word (m <= 8, rw words)
+PCUB_HD uint32_t packed_bits(const uint32_t* w, int s, int m, int rw) {
+    if (m <= 0) return 0u;
+    const int wi = s >> 5, sh = s & 31;
+    uint64_t x = w[wi];
+    if (sh + m > 32 && wi + 1 < rw) x |= (uint64_t)w[wi + 1] << 32;
+    return (uint32_t)(x >> sh) & ((1u << m) - 1u);
+}
+
+template <int N0, int TB>
+__global__ __launch_bounds__(kDelBlock) void k_sc_del_dense(DelArgs A) {
+    constexpr int L = 1 << N0, T = 1 << TB, G = kDenseG, LV = T / G, CPB = kDenseCPB;
+    constexpr int NW = T > 64 ? T / 64 : 1;
+    constexpr int WPC = (T * L + 31) / 32;
+    constexpr int ROW = N0 == 2 ? kN02Row : kN03Row;
+    constexpr int TL = TB - 4;  // descent levels below the lane's shared prefix
+    constexpr uint64_t WM = T >= 64 ? ~0ull : ((1ull << T) - 1ull);
+    static_assert((N0 == 2 || N0 == 3) && TB >= 4 && TB <= 8, "dense deletion: n0 2, 3 and 16 .. 256 trellises");
+    __shared__ double tab2[N0 == 2 ? kN02States * kN02Row : 1];
+    __shared__ uint32_t xs[CPB * WPC];
+    extern __shared__ uint32_t rxb[];
+    const double* tab;  // n0 = 3: the caller's table, registered for this pd (sc_del.hip)
+    if constexpr (N0 == 2) {
+        // once per workgroup (persistent launch)
+        for (int i = threadIdx.x; i < kN02States * 5; i += kDelBlock)
+            n02_table_entry(i / 5, i % 5, A.pd, tab2 + (i / 5) * kN02Row);
+        tab = tab2;
+    } else {
+        tab = A.tab3;
+    }
+    const int lane = threadIdx.x & 63;
+    const int j = threadIdx.x & (G - 1);
+    const int g = threadIdx.x / G;
+    const uint32_t jr = bitrev((uint32_t)j, 4);
+    const long long ngrp = (A.B + CPB - 1) / CPB;
+#pragma unroll 1
+    for (long long grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+        const long long cw = grp * CPB + g;
+        const bool valid = cw < A.B;
+        const long long c = valid ? cw : A.B - 1;  // padding codewords decode a duplicate, store nothing
+        for (int i = threadIdx.x; i < CPB * WPC; i += kDelBlock) xs[i] = 0;
+        // received words bit-packed into LDS (as k_sc_del: coalesced bytes, a ballot per 64)
+        for (int gg = threadIdx.x >> 6; gg < CPB; gg += kDelBlock / 64) {
+            long long cg = grp * CPB + gg;
+            cg = cg < A.B ? cg : A.B - 1;
+            const uint8_t* row = A.rx + cg * (long long)A.stride;
+            int ln = A.rx_len[cg];
+            ln = ln < 0 ? 0 : (ln > A.stride ? A.stride : ln);
+            for (int base = 0; base < A.rw * 32; base += 64) {
+                const int i = base + lane;
+                const unsigned long long msk = __ballot(i < ln && row[i] == 1);
+                const int wi = (base >> 5) + (lane & 1);
+                if (lane < 2 && wi < A.rw) rxb[gg * A.rw + wi] = (uint32_t)(msk >> (32 * lane));
+            }
+        }
+        __syncthreads();
+
+        // segments (removeDeletionGuardBands' descent): trellis tr = jr * 2^TL + i is reached by
+        // the 4 halvings of jr (shared by the lane's trellises), then the TL of i
+        const uint32_t* pw = rxb + g * A.rw;
+        int len = A.rx_len[c];
+        len = len < 0 ? 0 : (len > A.stride ? A.stride : len);
+        int sa[LV], se[LV];
+        {
+            int a = 0, e = len;
+            trim_range_packed(pw, a, e);
+#pragma unroll
+            for (int k = 3; k >= 0; --k) {
+                const int h = (e - a) / 2;
+                if ((jr >> k) & 1u) a += h;
+                else e = a + h;
+                trim_range_packed(pw, a, e);
+            }
+            sa[0] = a;
+            se[0] = e;
+        }
+#pragma unroll
+        for (int lev = 0; lev < TL; ++lev) {
+#pragma unroll
+            for (int i = (1 << lev) - 1; i >= 0; --i) {
+                const int a = sa[i], e = se[i], h = (e - a) / 2;
+                int la = a, le = a + h, ra = a + h, re = e;
+                trim_range_packed(pw, la, le);
+                trim_range_packed(pw, ra, re);
+                sa[2 * i] = la;
+                se[2 * i] = le;
+                sa[2 * i + 1] = ra;
+                se[2 * i + 1] = re;
+            }
+        }
+        // local value t (position j + 16 t) is trellis jr * 2^TL + bitrev(t): its state's row
+        int row[LV];
+#pragma unroll
+        for (int t = 0; t < LV; ++t) {
+            const int i = cbitrev(t, TL);
+            const int s = sa[i], m = se[i] - sa[i];
+            const uint32_t y = m <= L ? packed_bits(pw, s, m, A.rw) : 0u;
+            row[t] = (N0 == 2 ? n02_state(m, y) : n03_state(m, y)) * ROW;
+        }
+
+        // the walk: 2^n0 memoryless subtrees, input k of each trellis from its row and history
+        uint32_t hist[LV];
+#pragma unroll
+        for (int t = 0; t < LV; ++t) hist[t] = 0;
+        uint32_t acc = 0;
+        int nacc = 0, infow = 0;
+#pragma unroll 1
+        for (int k = 0; k < L; ++k) {
+            uint64_t fm[NW], fv[NW], ub[NW];
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const int us = k * T + 64 * w;
+                if constexpr (T >= 64) {
+                    fm[w] = (uint64_t)A.fmask[us >> 5] | ((uint64_t)A.fmask[(us >> 5) + 1] << 32);
+                    fv[w] = (uint64_t)A.fval[us >> 5] | ((uint64_t)A.fval[(us >> 5) + 1] << 32);
+                } else {
+                    fm[w] = (uint64_t)((A.fmask[us >> 5] >> (us & 31)) & (uint32_t)WM);
+                    fv[w] = (uint64_t)((A.fval[us >> 5] >> (us & 31)) & (uint32_t)WM);
+                }
+                ub[w] = 0;
+            }
+            bool rate0 = true;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) rate0 = rate0 && (fm[w] == WM);
+            uint32_t bits;
+            if (rate0) {  // decisions = the frozen values (wave-uniform)
+                bits = WinTree<LV, G, NW>::frozen(ub, fv, j);
+            } else {
+                double v[LV];
+#pragma unroll
+                for (int t = 0; t < LV; ++t) v[t] = tab[row[t] + dense_slot<N0>(k, hist[t])];
+                if constexpr (NW == 1) bits = WinTree<LV, G, 1>::run(v, ub, fm, fv, lane);
+                else bits = DelWin<LV, NW>::run(v, ub, fm, fv, lane);
+            }
+#pragma unroll
+            for (int t = 0; t < LV; ++t) hist[t] |= ((bits >> t) & 1u) << k;
+            // information bits in u order (lane j = 0 holds the subtree's decisions)
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                for (uint64_t im = ~fm[w] & WM; im != 0ull; im &= im - 1ull) {
+                    acc |= (uint32_t)((ub[w] >> __builtin_ctzll(im)) & 1ull) << nacc;
+                    if (++nacc == 32) {
+                        if (valid && j == 0 && A.info) A.info[(long long)infow * A.B + cw] = acc;
+                        acc = 0;
+                        nacc = 0;
+                        ++infow;
+                    }
+                }
+            }
+        }
+        if (nacc && valid && j == 0 && A.info) A.info[(long long)infow * A.B + cw] = acc;
+
+        // x_hat: trellis tr's slice is natural positions [tr L, (tr + 1) L) (L <= 8: one word)
+#pragma unroll
+        for (int t = 0; t < LV; ++t) {
+            const int pos = (int)((jr << TL) | (uint32_t)cbitrev(t, TL)) * L;
+            atomicOr(&xs[g * WPC + (pos >> 5)], enc_hist<L>(hist[t]) << (pos & 31));
+        }
+        __syncthreads();
+        if (A.xhat && valid)
+            for (int i = j; i < WPC; i += G) A.xhat[(long long)i * A.B + cw] = xs[g * WPC + i];
+        __syncthreads();  // xs / rxb are reused by the workgroup's next group
+    }
+}
+
+DelKern del_kernel_dense(int n0, int tb);  // sc_del_dense.hip; nullptr outside n0 2, 3 and tb 4 .. 8
+
+}  // namespace pcub

@@ -602,6 +602,12 @@ def leaf_deletion_supported(n, n0, ones=0):
     return bool(_lib.lib().pcub_sc_leaf_deletion_supported(int(n), int(n0), int(ones)))
 
 
+def set_deletion_dense(on):
+    """Allow (default) or forbid the table-driven deletion layout (pcub_sc_set_deletion_dense);
+    returns the previous setting.  Decisions are identical either way."""
+    return bool(_lib.lib().pcub_sc_set_deletion_dense(1 if on else 0))
+
+
 class DeletionDecoder:
     """Batched SC decoder over the deletion channel (CollectionOfBinaryTrellises built from
     each received word with buildCollectionOfBinaryTrellises_uniformInput_deletion, with

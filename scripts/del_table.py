@@ -1,5 +1,6 @@
-"""n0 = 3 deletion decode with and without the segment-state table (pcub_sc_deletion_build_table):
-throughput at n = 9..11 (main_deletion.py's n0 = n // 3).  Diagnostic, not a test."""
+"""Deletion decode layouts: n0 = 3 without the table (per-lane trellis levels), k_sc_del with the
+table, and the table-driven 16-lanes-a-codeword layout (sc_del_dense.h); n0 = 2 lane vs dense.
+Throughput at main_deletion.py's n0 = n // 3 shapes.  Diagnostic, not a test."""
 import os
 import sys
 
@@ -12,24 +13,31 @@ from scripts.del_split import timed  # noqa: E402
 
 
 def main():
-    pd, xi, n0 = 0.1, 0.1, 3
+    pd, xi = 0.1, 0.1
     dev = torch.device("cuda", 0)
-    for n in (9, 10, 11):
+    for n0, n, B in ((2, 8, 1 << 20), (2, 10, 1 << 18), (3, 9, 1 << 18), (3, 10, 1 << 18), (3, 11, 1 << 16)):
         N = 1 << n
-        B = 1 << (17 if n < 11 else 16)
         code = sc.CodeSpec.from_frozen_set(N, set(range(N - N // 4)), 200, device=dev)
         gen = torch.Generator(device=dev)
         gen.manual_seed(n)
         rx, ln, _ = mc.deletion_batch(code, B, n0, xi, pd, gen)
-        res = {}
-        for tab in (False, True):
+        res, outs = {}, {}
+        modes = (("plain", False, False), ("lane+tab", True, False), ("dense", True, True)) if n0 == 3 else \
+            (("lane", True, False), ("dense", True, True))
+        for name, tab, dense in modes:
+            if n0 == 3 and not tab and n >= 11:
+                continue
+            prev = sc.set_deletion_dense(dense)
             d = sc.DeletionDecoder(code, n0, pd, use_table=tab)
-            res[tab] = timed(d, rx, ln, reps=3)
+            res[name] = timed(d, rx, ln, reps=3)
             i0, x0 = d.decode_native(rx, ln)
-            res[(tab, "out")] = (i0.clone(), x0.clone())
-        same = all(torch.equal(a, b) for a, b in zip(res[(False, "out")], res[(True, "out")]))
-        print("n=%2d n0=3 B=%d  plain %8.2f ms %7.3f M cw/s | table %8.2f ms %7.3f M cw/s | identical %s"
-              % (n, B, res[False], B / res[False] / 1e3, res[True], B / res[True] / 1e3, same), flush=True)
+            outs[name] = (i0.clone(), x0.clone())
+            sc.set_deletion_dense(prev)
+        ref = outs["dense"]
+        same = all(torch.equal(a, b) for o in outs.values() for a, b in zip(o, ref))
+        print("n=%2d n0=%d B=%7d  " % (n, n0, B) + " | ".join("%s %8.2f ms %8.3f M cw/s" % (k, v, B / v / 1e3)
+                                                       for k, v in res.items()) + " | identical %s" % same,
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -134,9 +134,9 @@ def test_facade_dispatch_and_mc_line():
 
 @pytest.mark.parametrize("n", [5, 10, 11])
 def test_n03_table_paths_agree(sc, n):
-    """n0 = 3: the segment-state table (pcub_sc_deletion_build_table), the per-lane trellis
-    levels (no table) and a table built for another pd (its stamp does not match: the kernel
-    ignores it) decode identically, and agree with the oracle."""
+    """n0 = 3: the segment-state table (pcub_sc_deletion_build_table, the table-driven layout), the
+    per-lane trellis levels (no table) and a table built for another pd (not registered for this
+    pd: k_sc_del, whose stamp check ignores it) decode identically, and agree with the oracle."""
     n0, pd = 3, 0.1
     N = 1 << n
     rng = np.random.default_rng(31 + n)
@@ -160,5 +160,40 @@ def test_n03_table_paths_agree(sc, n):
     for o in outs[1:]:
         assert np.array_equal(o[0], outs[0][0]) and np.array_equal(o[1], outs[0][1])
     for i in list(range(0, len(words), 7)) + [len(words) - 1]:
+        x_ref, i_ref = tro.decode_deletion(words[i], n, n0, pd, frozen, fval)
+        assert list(outs[0][0][i]) == i_ref and list(outs[0][1][i]) == x_ref, i
+
+
+@pytest.mark.parametrize("n0,n", [(2, 6), (2, 8), (2, 9), (2, 10), (3, 7), (3, 9), (3, 10), (3, 11)])
+def test_dense_layout_matches_lane_layout(sc, n0, n):
+    """The table-driven layout (16 lanes a codeword, sc_del_dense.h) and k_sc_del's lane-per-trellis
+    layout decode identically (a ragged batch: padding codewords in the last workgroup), and
+    agree with the oracle on a sample."""
+    N = 1 << n
+    pd = 0.1
+    rng = np.random.default_rng(7 * n + n0)
+    prng = random.Random(3 * n + n0)
+    frozen = (rng.random(N) < 0.6).astype(np.uint8)
+    frozen[: N // 8] = 1
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    words = []
+    for _ in range(37):
+        x = [int(b) for b in rng.integers(0, 2, N)]
+        words.append(tro.deletion_channel(tro.add_guard_bands(x, n, n0, 0.1, 0), pd, prng))
+    words += [[], [1], [0] * 5, [int(b) for b in rng.integers(0, 2, 2 * N)]]
+    rxt, ln = sc.pad_words(words)
+    code = sc.CodeSpec(N, frozen, fval, device="cuda")
+    d = sc.DeletionDecoder(code, n0, pd)
+    outs = []
+    for dense in (True, False):
+        prev = sc.set_deletion_dense(dense)
+        try:
+            info, xhat = d.decode(rxt, ln)
+            torch.cuda.synchronize()
+        finally:
+            sc.set_deletion_dense(prev)
+        outs.append((info.cpu().numpy(), xhat.cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    for i in list(range(0, len(words), 9)) + [len(words) - 3, len(words) - 1]:
         x_ref, i_ref = tro.decode_deletion(words[i], n, n0, pd, frozen, fval)
         assert list(outs[0][0][i]) == i_ref and list(outs[0][1][i]) == x_ref, i

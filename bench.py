@@ -231,6 +231,8 @@ class Deletion:
                                                                 self.B, self.n0, self.xi, self.pd, self.ones)
         self.info_tx = sc.unpack(info_w, self.K)
         self.outs = None
+        self.dense = self.dec.dense_layout(self.rx.shape[1], self.rx.device)
+        self.kernel = "k_sc_del_dense" if self.dense else "k_sc_del"
 
     def step(self):
         self.outs = self.dec.decode_native(self.rx, self.rx_len)
@@ -242,7 +244,8 @@ class Deletion:
         return float(self.rx_len.float().mean().item()) + 4 + self.N // 8 + self.K // 8
 
     def tag(self):
-        return "del_n%d_n0%d%s" % (self.n, self.n0, "_k%d" % self.K if self.K != 3 else "")
+        return "del_n%d_n0%d%s%s" % (self.n, self.n0, "_k%d" % self.K if self.K != 3 else "",
+                                     "_dense" if self.dense else "")
 
     def describe(self, world):
         return dict(

@@ -142,6 +142,9 @@ int64_t pcub_sc_deletion_table_bytes(int32_t n0);
 /* Diagnostics: allow (1, the default) or forbid (0) the table-driven layout, 16 lanes per codeword
  * (DESIGN 3.2); returns the previous setting.  Decisions are identical either way. */
 int pcub_sc_set_deletion_dense(int32_t on);
+/* 1 when pcub_sc_decode_deletion_tab would run the table-driven layout for this shape, received
+ * row stride, table and pd (diagnostics: which kernel a profile names). */
+int pcub_sc_deletion_dense_layout(int32_t n, int32_t n0, int32_t ones, int32_t stride, const double* table, double pd);
 int pcub_sc_deletion_build_table(int32_t n0, double pd, double* table, void* stream);
 int pcub_sc_decode_deletion_tab(const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n,
                                 int32_t n0, int32_t ones, double pd, const uint32_t* frozen_mask,

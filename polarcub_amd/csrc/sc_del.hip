@@ -102,6 +102,16 @@ OnesProbs ones_probs(int ones, double pd) {
     return op;
 }
 
+// the table-driven layout (sc_del_dense.h) when the stage has a table: n0 = 2 (built per
+// workgroup) or n0 = 3 with a table this library built for pd, no ones, 16 .. 256 trellises,
+// and the group's received words fit LDS bit-packed
+bool use_dense(int n, int n0, int ones, int stride, const double* table, double pd) {
+    const long long rw = ((long long)stride + 31) / 32;
+    return g_dense.load(std::memory_order_relaxed) && ones == 0 &&
+           (n0 == 2 || (n0 == 3 && tab_registered(table, pd))) && n - n0 >= 4 &&
+           (long long)kDenseCPB * rw * 4 <= kDenseMaxRxLds && del_kernel_dense(n0, n - n0) != nullptr;
+}
+
 int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n, int32_t n0,
                int32_t ones, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
                const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words, double* leaf,
@@ -131,11 +141,7 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     DelKern k = kern;
     long long cpb = kDelBlock >> (n - n0);
     const long long rw = ((long long)stride + 31) / 32;
-    // the table-driven layout (sc_del_dense.h) when the stage has a table: n0 = 2 (built per
-    // workgroup) or n0 = 3 with the caller's table, no ones, 16 .. 256 trellises, and the
-    // group's received words fit LDS bit-packed
-    const bool dense = g_dense.load(std::memory_order_relaxed) && !exp && ones == 0 && (n0 == 2 || (n0 == 3 && tab_registered(A.tab3, pd))) && n - n0 >= 4 &&
-                       (long long)kDenseCPB * rw * 4 <= kDenseMaxRxLds && del_kernel_dense(n0, n - n0);
+    const bool dense = !exp && use_dense(n, n0, ones, stride, table, pd);
     if (dense) {
         k = del_kernel_dense(n0, n - n0);
         cpb = kDenseCPB;
@@ -154,7 +160,10 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kDelBlock, lds) == hipSuccess && cus > 0 &&
             occ > 0) {
-            const long long res = (long long)cus * occ;
+            // the occupancy API reports one workgroup a CU too many for 256-thread blocks at 97 .. 112
+            // SGPRs (MI355X_MICROARCH.md, occupancy row): 800 / (112 + 16) = 6 waves a SIMD at most,
+            // and an over-size persistent grid leaves its last workgroups to run after the others
+            const long long res = (long long)cus * (occ < 6 ? occ : 6);
             if (grid > res) grid = res;
         }
     }
@@ -210,6 +219,12 @@ extern "C" int pcub_sc_leaf_deletion_tab(const uint8_t* rx, const int32_t* rx_le
 
 extern "C" int pcub_sc_set_deletion_dense(int32_t on) {
     return g_dense.exchange(on ? 1 : 0);
+}
+
+extern "C" int pcub_sc_deletion_dense_layout(int32_t n, int32_t n0, int32_t ones, int32_t stride, const double* table,
+                                             double pd) {
+    return del_kernel(n0, n - n0, false, ones) != nullptr && stride >= 0 && stride <= 32767 &&
+           use_dense(n, n0, ones, stride, table, pd);
 }
 
 extern "C" int64_t pcub_sc_deletion_table_bytes(int32_t n0) {

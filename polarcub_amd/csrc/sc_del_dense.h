@@ -98,20 +98,7 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del_dense(DelArgs A) {
         const bool valid = cw < A.B;
         const long long c = valid ? cw : A.B - 1;  // padding codewords decode a duplicate, store nothing
         for (int i = threadIdx.x; i < CPB * WPC; i += kDelBlock) xs[i] = 0;
-        // received words bit-packed into LDS (as k_sc_del: coalesced bytes, a ballot per 64)
-        for (int gg = threadIdx.x >> 6; gg < CPB; gg += kDelBlock / 64) {
-            long long cg = grp * CPB + gg;
-            cg = cg < A.B ? cg : A.B - 1;
-            const uint8_t* row = A.rx + cg * (long long)A.stride;
-            int ln = A.rx_len[cg];
-            ln = ln < 0 ? 0 : (ln > A.stride ? A.stride : ln);
-            for (int base = 0; base < A.rw * 32; base += 64) {
-                const int i = base + lane;
-                const unsigned long long msk = __ballot(i < ln && row[i] == 1);
-                const int wi = (base >> 5) + (lane & 1);
-                if (lane < 2 && wi < A.rw) rxb[gg * A.rw + wi] = (uint32_t)(msk >> (32 * lane));
-            }
-        }
+        pack_rows<CPB>(A, grp, rxb, lane);  // received words bit-packed into LDS (sc_del_kern.h)
         __syncthreads();
 
         // segments (removeDeletionGuardBands' descent): trellis tr = jr * 2^TL + i is reached by

@@ -563,6 +563,38 @@ __device__ __forceinline__ uint32_t del_n02(const Base02& b, DelCtx<T, EXP>& cx)
     return x;
 }
 
+// The group's received words, bit-packed into LDS (bit i of word i >> 5 of row gg = symbol i
+// is 1): each wave packs whole rows with coalesced byte loads and a ballot per 64 symbols, kPackU
+// loads in flight before the first ballot (one dependent HBM round trip per kPackU * 64
+// symbols, not per 64).
+constexpr int kPackU = 16;
+
+template <int CPB>
+__device__ __forceinline__ void pack_rows(const DelArgs& A, long long grp, uint32_t* rxb, int lane) {
+    const int nch = (A.rw * 32 + 63) / 64;  // 64-symbol chunks per row
+    for (int gg = threadIdx.x >> 6; gg < CPB; gg += kDelBlock / 64) {
+        long long cg = grp * CPB + gg;
+        cg = cg < A.B ? cg : A.B - 1;
+        const uint8_t* row = A.rx + cg * (long long)A.stride;
+        int ln = A.rx_len[cg];
+        ln = ln < 0 ? 0 : (ln > A.stride ? A.stride : ln);
+        for (int c0 = 0; c0 < nch; c0 += kPackU) {
+            uint32_t b[kPackU];
+#pragma unroll
+            for (int u = 0; u < kPackU; ++u) {
+                const int i = (c0 + u) * 64 + lane;
+                b[u] = i < ln ? (uint32_t)row[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kPackU; ++u) {
+                const unsigned long long msk = __ballot(b[u] == 1u);
+                const int wi = 2 * (c0 + u) + (lane & 1);
+                if (lane < 2 && wi < A.rw) rxb[gg * A.rw + wi] = (uint32_t)(msk >> (32 * lane));
+            }
+        }
+    }
+}
+
 template <int N0, int TB, bool EXP, int OC>
 __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint32_t* xs, const double* n02tab) {
     constexpr int L = 1 << N0;
@@ -587,19 +619,7 @@ __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint3
     extern __shared__ uint32_t rxb[];
     const bool pk = A.rw > 0;
     if (pk) {
-        for (int gg = threadIdx.x >> 6; gg < CPB; gg += kDelBlock / 64) {
-            long long cg = grp * CPB + gg;
-            cg = cg < A.B ? cg : A.B - 1;
-            const uint8_t* row = A.rx + cg * (long long)A.stride;
-            int ln = A.rx_len[cg];
-            ln = ln < 0 ? 0 : (ln > A.stride ? A.stride : ln);
-            for (int base = 0; base < A.rw * 32; base += 64) {
-                const int i = base + lane;
-                const unsigned long long msk = __ballot(i < ln && row[i] == 1);
-                const int wi = (base >> 5) + (lane & 1);
-                if (lane < 2 && wi < A.rw) rxb[gg * A.rw + wi] = (uint32_t)(msk >> (32 * lane));
-            }
-        }
+        pack_rows<CPB>(A, grp, rxb, lane);
         __syncthreads();
     }
 

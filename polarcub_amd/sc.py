@@ -643,6 +643,12 @@ class DeletionDecoder:
             self._tables[key] = t
         return t
 
+    def dense_layout(self, stride, device):
+        """True when decodes of rows of `stride` symbols run the table-driven layout
+        (k_sc_del_dense) rather than k_sc_del."""
+        return bool(_lib.lib().pcub_sc_deletion_dense_layout(self.code.n, self.n0, self.ones, int(stride),
+                                                             _p(self.table(device)), self.pd))
+
     def decode_native(self, rx, rx_len, want_xhat=True):
         """rx: [B, W] uint8 received symbols on device, rx_len: [B] int32.
         Returns packed (info_words [ceil(K/32), B], xhat_words [ceil(N/32), B] | None)."""

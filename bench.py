@@ -120,9 +120,10 @@ class Awgn:
 
     def end_to_end(self):
         """The whole Monte-Carlo pipeline on the device (pcub_mc_run_bin: information bits ->
-        encoder -> BI-AWGN -> decode -> counters) over this rank's codewords, in chunks of up to
-        2^20 codewords: seconds of the second (warm: workspace cached) run."""
-        chunk = min(self.B, 1 << 20)
+        encoder -> BI-AWGN -> decode -> counters) over this rank's codewords, in chunks of 2^18
+        codewords (chunk i+1's generation overlaps chunk i's decode): seconds of the second (warm:
+        workspace cached) run."""
+        chunk = min(self.B, 1 << 18)
         mc.run_bin(self.code, self.a.seed, self.offset, self.B, mc.CHANNEL_AWGN, self.sigma2, chunk=chunk)
         torch.cuda.synchronize()
         t0 = time.perf_counter()

@@ -14,6 +14,9 @@
 // driver (coding.encodeDecodeSimulation), which replays the reference's RNGs.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+
 #include "polarcub_sc.h"
 #include "sc_common.h"
 
@@ -416,8 +419,10 @@ namespace {
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// Two generation slots (information words, compact channel rows), so the generation of chunk i+1
+// on a side stream overlaps the decode of chunk i on the caller's; one x and one decision buffer.
 struct McLayout {
-    size_t info, x, xy, dec, dws, total;
+    size_t info[2], x, xy[2], dec, dws, total;
 };
 
 McLayout mc_layout(int64_t chunk, int32_t log2N, int32_t K) {
@@ -425,13 +430,30 @@ McLayout mc_layout(int64_t chunk, int32_t log2N, int32_t K) {
     const size_t N = (size_t)1 << log2N;
     const size_t iw = (size_t)((K + 31) / 32 > 0 ? (K + 31) / 32 : 1);
     const size_t nw = (N + 31) / 32;
-    L.info = 0;
-    L.x = L.info + align256(iw * chunk * 4);
-    L.xy = L.x + align256(nw * chunk * 4);
-    L.dec = L.xy + align256(N * chunk * 16);
+    L.info[0] = 0;
+    L.info[1] = L.info[0] + align256(iw * chunk * 4);
+    L.x = L.info[1] + align256(iw * chunk * 4);
+    L.xy[0] = L.x + align256(nw * chunk * 4);
+    L.xy[1] = L.xy[0] + align256(N * chunk * 8);
+    L.dec = L.xy[1] + align256(N * chunk * 8);
     L.dws = L.dec + align256(iw * chunk * 4);
     L.total = L.dws + align256(pcub_sc_decode_bin_compact_workspace(chunk, log2N));
     return L;
+}
+
+// the side stream of each device (created on first use, kept for the process)
+hipStream_t gen_stream() {
+    static std::mutex mu;
+    static std::map<int, hipStream_t> streams;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = streams.find(dev);
+    if (it != streams.end()) return it->second;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    streams[dev] = s;
+    return s;
 }
 
 }  // namespace
@@ -448,21 +470,64 @@ extern "C" int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int
     const McLayout L = mc_layout(chunk, log2N, K);
     if (!workspace || workspace_bytes < L.total) return PCUB_EINVAL;
     char* ws = (char*)workspace;
-    uint32_t* info = (uint32_t*)(ws + L.info);
     uint32_t* x = (uint32_t*)(ws + L.x);
-    double* xy = (double*)(ws + L.xy);
     uint32_t* dec = (uint32_t*)(ws + L.dec);
-    for (int64_t c0 = 0; c0 < count; c0 += chunk) {
-        const int64_t B = (count - c0) < chunk ? (count - c0) : chunk;
-        int rc;
-        if (K > 0 && (rc = pcub_mc_info(seed, offset + c0, B, K, info, stream))) return rc;
-        if ((rc = pcub_polar_encode_bin(info, B, log2N, frozen_mask, frozen_val, K, x, stream))) return rc;
-        // normalised rows in compact form (8 bytes a position) into the compact-root decode
-        if ((rc = pcub_mc_channel_norm(seed, offset + c0, B, log2N, channel, param, x, xy, 1, stream))) return rc;
-        if ((rc = pcub_sc_decode_bin_compact(xy, B, log2N, frozen_mask, frozen_val, K, dec, nullptr, nullptr,
-                                             ws + L.dws, L.total - L.dws, stream)))
-            return rc;
-        if ((rc = pcub_mc_count_errors(dec, info, B, K, counters, stream))) return rc;
+    const hipStream_t ms = (hipStream_t)stream;
+    const int64_t nchunk = count == 0 ? 0 : (count + chunk - 1) / chunk;
+    // chunk i's generation (info -> encode -> channel rows into slot i % 2) runs on the side stream
+    // and overlaps chunk i-1's decode on the caller's stream; slot reuse waits for the decode and
+    // the counting of chunk i-2.  One chunk: everything on the caller's stream.
+    const hipStream_t gs = nchunk > 1 ? gen_stream() : ms;
+    if (nchunk > 1 && !gs) return (int)hipErrorInvalidResourceHandle;  // (ms may be the null stream)
+    hipEvent_t start = nullptr, ready[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
+    int rc = 0;
+    auto mk = [&](hipEvent_t* e) {
+        if (!rc) rc = (int)hipEventCreateWithFlags(e, hipEventDisableTiming);
+    };
+    if (gs != ms) {
+        mk(&start);
+        for (int i = 0; i < 2; ++i) {
+            mk(&ready[i]);
+            mk(&freed[i]);
+        }
+        if (!rc) rc = (int)hipEventRecord(start, ms);  // the caller's earlier work first
+        if (!rc) rc = (int)hipStreamWaitEvent(gs, start, 0);
     }
-    return 0;
+    auto gen = [&](int64_t i) -> int {
+        const int64_t c0 = i * chunk, B = (count - c0) < chunk ? (count - c0) : chunk;
+        const int k = (int)(i & 1);
+        uint32_t* info = (uint32_t*)(ws + L.info[k]);
+        double* xy = (double*)(ws + L.xy[k]);
+        int r;
+        if (gs != ms && i >= 2 && (r = (int)hipStreamWaitEvent(gs, freed[k], 0))) return r;
+        if (K > 0 && (r = pcub_mc_info(seed, offset + c0, B, K, info, gs))) return r;
+        if ((r = pcub_polar_encode_bin(info, B, log2N, frozen_mask, frozen_val, K, x, gs))) return r;
+        // normalised rows in compact form (8 bytes a position) into the compact-root decode
+        if ((r = pcub_mc_channel_norm(seed, offset + c0, B, log2N, channel, param, x, xy, 1, gs))) return r;
+        if (gs != ms && (r = (int)hipEventRecord(ready[k], gs))) return r;
+        return 0;
+    };
+    for (int64_t i = 0; !rc && i < nchunk; ++i) {
+        const int64_t c0 = i * chunk, B = (count - c0) < chunk ? (count - c0) : chunk;
+        const int k = (int)(i & 1);
+        if (i == 0) rc = gen(0);
+        if (!rc && i + 1 < nchunk) rc = gen(i + 1);  // enqueued before this chunk's decode
+        if (rc) break;
+        if (gs != ms && (rc = (int)hipStreamWaitEvent(ms, ready[k], 0))) break;
+        if ((rc = pcub_sc_decode_bin_compact((const double*)(ws + L.xy[k]), B, log2N, frozen_mask, frozen_val, K,
+                                             dec, nullptr, nullptr, ws + L.dws, L.total - L.dws, ms)))
+            break;
+        if ((rc = pcub_mc_count_errors(dec, (const uint32_t*)(ws + L.info[k]), B, K, counters, ms))) break;
+        if (gs != ms && (rc = (int)hipEventRecord(freed[k], ms))) break;
+    }
+    if (gs != ms && rc) {  // nothing of this call may still run on the side stream after it returns
+        hipEvent_t done = nullptr;
+        if (hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess) {
+            if (hipEventRecord(done, gs) == hipSuccess) (void)hipStreamWaitEvent(ms, done, 0);
+            (void)hipEventDestroy(done);
+        }
+    }
+    for (hipEvent_t e : {start, ready[0], ready[1], freed[0], freed[1]})
+        if (e) (void)hipEventDestroy(e);
+    return rc;
 }

@@ -118,18 +118,21 @@ class Awgn:
         d = sc.unpack(self.outs[0], self.K)
         return mc.error_counts(d, sc.unpack(self.info_w, self.K))
 
-    def end_to_end(self):
+    def end_to_end(self, reps=3):
         """The whole Monte-Carlo pipeline on the device (pcub_mc_run_bin: information bits ->
         encoder -> BI-AWGN -> decode -> counters) over this rank's codewords, in chunks of 2^18
-        codewords (chunk i+1's generation overlaps chunk i's decode): seconds of the second (warm:
-        workspace cached) run."""
-        chunk = min(self.B, 1 << 18)
+        codewords (chunk i+1's generation overlaps chunk i's decode): seconds of the median of
+        `reps` warm runs (a single ~20 ms run varies by +-10 % with the two streams' interleaving)."""
+        chunk = min(self.B, self.a.e2e_chunk)
         mc.run_bin(self.code, self.a.seed, self.offset, self.B, mc.CHANNEL_AWGN, self.sigma2, chunk=chunk)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        mc.run_bin(self.code, self.a.seed, self.offset, self.B, mc.CHANNEL_AWGN, self.sigma2, chunk=chunk)
-        torch.cuda.synchronize()
-        return time.perf_counter() - t0
+        times = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            mc.run_bin(self.code, self.a.seed, self.offset, self.B, mc.CHANNEL_AWGN, self.sigma2, chunk=chunk)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        return float(np.median(times))
 
     def bytes_alg(self):
         return 16 * self.N + self.N // 8 + self.K // 8  # f64 pairs in + packed x_hat + packed info
@@ -537,6 +540,8 @@ def build_parser():
     ap.add_argument("--master-port", type=int, default=0, help="rendezvous port when launching ranks (0 = free port)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-xhat", action="store_true")
+    ap.add_argument("--e2e-chunk", type=int, default=1 << 18,
+                    help="codewords per chunk of the end-to-end Monte-Carlo line (generation overlaps decode)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end Monte-Carlo leg (profiling: only the timed decode launches)")
     return ap
@@ -665,7 +670,8 @@ def main(argv=None):
         if e2e is not None:
             rec["mc_end_to_end"] = {"value": e2e, "unit": "codewords/s",
                                     "what": "pcub_mc_run_bin: info bits + encode + channel + decode + counters, "
-                                            "all on device, same codewords"}
+                                            "all on device, same codewords; chunks of %d, median of 3 warm runs"
+                                            % min(w.B, a.e2e_chunk)}
         if world == 1 and not a.no_cpu and hasattr(w, "cpu_baseline"):
             rec["cpu_baseline"] = w.cpu_baseline()
         print(json.dumps(rec), flush=True)

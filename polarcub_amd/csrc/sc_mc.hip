@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_
         if (A.channel == 0) {
             const double rad = sqrt(-2.0 * log(u0));
             double sn, cs;
-            sincos(6.283185307179586 * u1, &sn, &cs);
+            sincospi(2.0 * u1, &sn, &cs);  // sin, cos of 2 pi u1 (pi-scaled reduction)
             o0 = awgn_pair(A, xw & 1u, rad * cs);
             o1 = awgn_pair(A, (xw >> 1) & 1u, rad * sn);
         } else {
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel_norm(McArgs A, const ui
         if (A.channel == 0) {
             const double rad = sqrt(-2.0 * log(u0));
             double sn, cs;
-            sincos(6.283185307179586 * u1, &sn, &cs);
+            sincospi(2.0 * u1, &sn, &cs);  // sin, cos of 2 pi u1 (pi-scaled reduction)
             c0 = awgn_norm(A, xw & 1u, rad * cs);
             c1 = awgn_norm(A, (xw >> 1) & 1u, rad * sn);
         } else {

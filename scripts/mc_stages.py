@@ -16,10 +16,18 @@ n, K, B = 10, 512, 1 << 20
 s2 = construction.awgn_sigma2(2.0, K / (1 << n))
 fr = construction.bhattacharyya_frozen(n, K, s2)
 code = sc.CodeSpec.from_frozen_set(1 << n, set(np.nonzero(fr)[0].tolist()), 1, device=torch.device("cuda", 0))
-for rep, chunk in [(r, c) for c in chunks for r in range(2)]:
+reps = int(os.environ.get("REPS", "2"))
+res = {c: [] for c in chunks}
+for rep, chunk in [(r, c) for r in range(reps) for c in chunks]:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     c = mc.run_bin(code, 1, 0, B, mc.CHANNEL_AWGN, s2, chunk=chunk)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     print("chunk %d: %.2f ms  %.1f M cw/s  counters %s" % (chunk, dt * 1e3, B / dt / 1e6, c), flush=True)
+    if rep > 0:
+        res[chunk].append(B / dt / 1e6)
+for c, v in res.items():
+    if v:
+        print("chunk %d: median %.1f M cw/s over %d runs (min %.1f, max %.1f)" % (c, float(np.median(v)), len(v),
+                                                                            min(v), max(v)))

@@ -131,6 +131,10 @@ bool fits(int v, int n) {
 }
 int pick_variant(int n) {
     if (fits(g_variant, n)) return g_variant;
+    // past the split level's LDS budget with the bits in LDS (N = 4096, 8192): the split level with
+    // the bits in scratch, one stored depth fewer (N = 4096 13.1 -> 14.1 M cw/s, N = 8192 5.2 -> 5.7 M;
+    // equal at N = 16384, where variant 17 stays)
+    if (n <= 13 && g_variant == kDefaultVariant && fits(31, n)) return 31;
     constexpr int kFallback[] = {24, 17, 13, 14, 10, 0, 1};
     for (int v : kFallback)
         if (fits(v, n)) return v;

@@ -66,6 +66,39 @@ PCUB_HD uint32_t packed_bits(const uint32_t* w, int s, int m, int rw) {
     return (uint32_t)(x >> sh) & ((1u << m) - 1u);
 }
 
+// The segments of the 2^(TB-4) trellises tr = jr * 2^(TB-4) + i of one lane (removeDeletionGuardBands'
+// descent, segment_of_packed): the 4 halvings of jr, shared by them, then a split per level, each
+// range halved and both halves trimmed; entry i = [sa[i], se[i]).
+template <int TB>
+PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, int* se) {
+    constexpr int TL = TB - 4;
+    int a = 0, e = len;
+    trim_range_packed(pw, a, e);
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+        const int h = (e - a) / 2;
+        if ((jr >> k) & 1u) a += h;
+        else e = a + h;
+        trim_range_packed(pw, a, e);
+    }
+    sa[0] = a;
+    se[0] = e;
+#pragma unroll
+    for (int lev = 0; lev < TL; ++lev) {
+#pragma unroll
+        for (int i = (1 << lev) - 1; i >= 0; --i) {
+            const int a0 = sa[i], e0 = se[i], h = (e0 - a0) / 2;
+            int la = a0, le = a0 + h, ra = a0 + h, re = e0;
+            trim_range_packed(pw, la, le);
+            trim_range_packed(pw, ra, re);
+            sa[2 * i] = la;
+            se[2 * i] = le;
+            sa[2 * i + 1] = ra;
+            se[2 * i + 1] = re;
+        }
+    }
+}
+
 template <int N0, int TB>
 __global__ __launch_bounds__(kDelBlock) void k_sc_del_dense(DelArgs A) {
     constexpr int L = 1 << N0, T = 1 << TB, G = kDenseG, LV = T / G, CPB = kDenseCPB;
@@ -107,33 +140,7 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del_dense(DelArgs A) {
         int len = A.rx_len[c];
         len = len < 0 ? 0 : (len > A.stride ? A.stride : len);
         int sa[LV], se[LV];
-        {
-            int a = 0, e = len;
-            trim_range_packed(pw, a, e);
-#pragma unroll
-            for (int k = 3; k >= 0; --k) {
-                const int h = (e - a) / 2;
-                if ((jr >> k) & 1u) a += h;
-                else e = a + h;
-                trim_range_packed(pw, a, e);
-            }
-            sa[0] = a;
-            se[0] = e;
-        }
-#pragma unroll
-        for (int lev = 0; lev < TL; ++lev) {
-#pragma unroll
-            for (int i = (1 << lev) - 1; i >= 0; --i) {
-                const int a = sa[i], e = se[i], h = (e - a) / 2;
-                int la = a, le = a + h, ra = a + h, re = e;
-                trim_range_packed(pw, la, le);
-                trim_range_packed(pw, ra, re);
-                sa[2 * i] = la;
-                se[2 * i] = le;
-                sa[2 * i + 1] = ra;
-                se[2 * i + 1] = re;
-            }
-        }
+        dense_segments<TB>(pw, len, jr, sa, se);
         // local value t (position j + 16 t) is trellis jr * 2^TL + bitrev(t): its state's row
         int row[LV];
 #pragma unroll

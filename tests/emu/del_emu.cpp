@@ -12,6 +12,7 @@
 
 #include "trellis_body.h"
 #include "trellis_n02.h"
+#include "sc_del_dense.h"
 #include "sc_del_kern.h"
 
 using namespace pcub;
@@ -390,5 +391,78 @@ extern "C" long long emu_check_segments(uint64_t seed, int words) {
                 bad += (s0 != s1 || m0 != m1) ? 1 : 0;
             }
     }
+    return bad;
+}
+
+// The table-driven layout's own host-visible pieces (sc_del_dense.h), against their definitions:
+// dense_segments (a lane's shared descent + per-level splits) = segment_of_packed for every trellis
+// of the lane, for 16..256 trellises; enc_hist<L> = DelNode's recursive re-encoding; dense_slot<2>
+// = the n02 table's layout for every history.  Returns the number of disagreements.
+namespace {
+uint32_t enc_ref(uint32_t h, int L) {  // DelNode: x[2i] = ym[i] ^ yp[i], x[2i+1] = yp[i]
+    if (L == 1) return h & 1u;
+    const int H = L / 2;
+    const uint32_t ym = enc_ref(h & ((1u << H) - 1u), H), yp = enc_ref(h >> H, H);
+    uint32_t x = 0;
+    for (int i = 0; i < H; ++i) x |= ((((ym ^ yp) >> i) & 1u) << (2 * i)) | (((yp >> i) & 1u) << (2 * i + 1));
+    return x;
+}
+
+template <int TB>
+long long dense_seg_check(const std::vector<uint32_t>& pk, int len) {
+    constexpr int LV = 1 << (TB - 4);
+    long long bad = 0;
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t jr = pcub::bitrev((uint32_t)j, 4);
+        int sa[LV], se[LV];
+        pcub::dense_segments<TB>(pk.data(), len, jr, sa, se);
+        for (int i = 0; i < LV; ++i) {
+            int s, m;
+            pcub::segment_of_packed(pk.data(), len, TB, (int)(jr << (TB - 4)) + i, s, m);
+            bad += (s != sa[i] || m != se[i] - sa[i]) ? 1 : 0;
+        }
+    }
+    return bad;
+}
+}  // namespace
+
+extern "C" long long emu_check_dense(uint64_t seed, int words) {
+    uint64_t st = seed * 0x9E3779B97F4A7C15ull + 7;
+    auto rnd = [&st]() {
+        st ^= st << 13;
+        st ^= st >> 7;
+        st ^= st << 17;
+        return st;
+    };
+    long long bad = 0;
+    for (int it = 0; it < words; ++it) {
+        const int len = (int)(rnd() % 4000);
+        std::vector<uint8_t> w(len + 1, 0);
+        int i = 0;
+        while (i < len) {
+            const int run = (int)(rnd() % (rnd() % 4 == 0 ? 120 : 4)) + 1;
+            const uint8_t v = (uint8_t)(rnd() % 3 == 0 ? 0 : (rnd() & 1));
+            for (int j = 0; j < run && i < len; ++j, ++i) w[i] = (rnd() % 5 == 0) ? (uint8_t)(rnd() & 1) : v;
+        }
+        std::vector<uint32_t> pk((len + 31) / 32 + 1, 0);
+        for (int j = 0; j < len; ++j)
+            if (w[j] == 1) pk[j >> 5] |= 1u << (j & 31);
+        bad += dense_seg_check<4>(pk, len) + dense_seg_check<5>(pk, len) + dense_seg_check<6>(pk, len) +
+               dense_seg_check<7>(pk, len) + dense_seg_check<8>(pk, len);
+    }
+    for (uint32_t h = 0; h < 256; ++h) {
+        bad += (pcub::enc_hist<8>(h) != enc_ref(h, 8)) ? 1 : 0;
+        if (h < 16) bad += (pcub::enc_hist<4>(h) != enc_ref(h, 4)) ? 1 : 0;
+    }
+    // dense_slot<2>: [0] v1, [1 + xm] v2, [3 + ym] v3, [7 + 2 ym + xm'] v4 (ym = (xm ^ xp) | xp << 1)
+    for (uint32_t h = 0; h < 8; ++h) {
+        const uint32_t xm = h & 1u, xp = (h >> 1) & 1u, ym = (xm ^ xp) | (xp << 1), xm2 = (h >> 2) & 1u;
+        bad += (pcub::dense_slot<2>(0, 0) != 0) ? 1 : 0;
+        bad += (pcub::dense_slot<2>(1, h & 1u) != 1 + (int)xm) ? 1 : 0;
+        bad += (pcub::dense_slot<2>(2, h & 3u) != 3 + (int)ym) ? 1 : 0;
+        bad += (pcub::dense_slot<2>(3, h) != 7 + 2 * (int)ym + (int)xm2) ? 1 : 0;
+    }
+    for (int k = 0; k < 8; ++k)
+        for (uint32_t h = 0; h < (1u << k); ++h) bad += (pcub::dense_slot<3>(k, h) != (1 << k) - 1 + (int)h) ? 1 : 0;
     return bad;
 }

@@ -118,6 +118,16 @@ def test_packed_segment_parse_matches_byte_parse():
     assert L.emu_check_segments(ctypes.c_uint64(12345), 3000) == 0
 
 
+def test_dense_layout_host_pieces():
+    """The table-driven layout (sc_del_dense.h): a lane's shared descent plus per-level splits
+    (dense_segments) gives segment_of_packed's segment for each of its trellises at 16..256
+    trellises on random words with long zero runs; enc_hist is DelNode's re-encoding; the history
+    slots are the n0 = 2 and n0 = 3 tables' layouts."""
+    L = emu()
+    L.emu_check_dense.restype = ctypes.c_longlong
+    assert L.emu_check_dense(ctypes.c_uint64(777), 600) == 0
+
+
 @pytest.fixture(params=[False, True], ids=["stored-base", "implicit-base"])
 def implicit_base(request):
     """n0 >= 3 without guard-band ones: the kernel never stores the base trellis (BaseT,

@@ -127,17 +127,18 @@ int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, i
                           const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
                           double* leaf, void* stream);
 
-/* n0 = 3 segment-state table (trellis depth 3, ones = 0): every value a trellis lane hands to
- * the memoryless subtree is a function of its segment (m <= 8 received bits) and of the bits
- * the subtree returned before it, so one 1 MiB table per pd replaces the per-lane trellis
- * levels.  pcub_sc_deletion_table_bytes(n0) is its size (0: no table for n0);
+/* Segment-state tables (n0 = 2: 4 KiB; n0 = 3: 1 MiB; ones = 0): every value a trellis hands to
+ * the memoryless subtree is a function of its segment (m <= 2^n0 received bits) and of the bits
+ * the subtree returned before it, so one table per pd replaces the per-lane trellis levels
+ * (DESIGN 3.2).  pcub_sc_deletion_table_bytes(n0) is its size (0: no table for n0);
  * pcub_sc_deletion_build_table fills it on the stream (8-byte aligned device memory).
- * The _tab twins of the two deletion entry points read it when n0 = 3 and ones = 0 and the
+ * The _tab twins of the two deletion entry points read it when n0 = 2 or 3 and ones = 0 and the
  * table was built for the same pd (its stamp); otherwise, or with table = NULL, they decode
- * as the plain entry points.  Decisions are identical either way.  The table must stay
- * allocated and unmodified while decodes that read it are in flight (ordinary stream rules:
- * build and decode on one stream, or synchronise); the library remembers (pointer, pd) of the
- * tables it built (the last 64) and runs the table-driven layout only on those. */
+ * as the plain entry points (n0 = 2 then builds its table per workgroup).  Decisions are
+ * identical either way.  The table must stay allocated and unmodified while decodes that read it
+ * are in flight (ordinary stream rules: build and decode on one stream, or synchronise); the
+ * library remembers (pointer, pd) of the tables it built (the last 64) and runs the table-driven
+ * layout from a table only on those. */
 int64_t pcub_sc_deletion_table_bytes(int32_t n0);
 /* Diagnostics: allow (1, the default) or forbid (0) the table-driven layout, 16 lanes per codeword
  * (DESIGN 3.2); returns the previous setting.  Decisions are identical either way. */

@@ -72,6 +72,13 @@ __global__ __launch_bounds__(256) void k_del_n03_table(double pd, double* tab) {
     tab[i] = n03_table_entry(st, k, (uint32_t)(j + 1 - (1 << k)), pd);
 }
 
+// the n0 = 2 table (trellis_n02.h): one thread per (state, child) row part, entry 15 of every row pd
+__global__ __launch_bounds__(256) void k_del_n02_table(double pd, double* tab) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < kN02States * 5) n02_table_entry(i / 5, i % 5, pd, tab + (i / 5) * kN02Row);
+    if (i < kN02States) tab[i * kN02Row + kN02Row - 1] = pd;
+}
+
 DelKern del_kernel(int n0, int tb, bool exp, int ones) {
     if (ones < 0 || ones > kMaxOnes) return nullptr;
     const int oc = ones > 0 ? kMaxOnes : 0;
@@ -137,13 +144,13 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     A.info = info_words;
     A.xhat = xhat_words;
     A.leaf = leaf;
-    A.tab3 = (n0 == 3 && ones == 0) ? table : nullptr;
+    A.tab = ((n0 == 2 || n0 == 3) && ones == 0) ? table : nullptr;
     DelKern k = kern;
     long long cpb = kDelBlock >> (n - n0);
     const long long rw = ((long long)stride + 31) / 32;
     const bool dense = !exp && use_dense(n, n0, ones, stride, table, pd);
     if (dense) {
-        k = del_kernel_dense(n0, n - n0);
+        k = del_kernel_dense(n0, n - n0, n0 == 2 && tab_registered(table, pd));
         cpb = kDenseCPB;
     }
     long long grid = (B + cpb - 1) / cpb;
@@ -228,13 +235,17 @@ extern "C" int pcub_sc_deletion_dense_layout(int32_t n, int32_t n0, int32_t ones
 }
 
 extern "C" int64_t pcub_sc_deletion_table_bytes(int32_t n0) {
+    if (n0 == 2) return (int64_t)kN02States * kN02Row * (int64_t)sizeof(double);
     return n0 == 3 ? (int64_t)kN03States * kN03Row * (int64_t)sizeof(double) : 0;
 }
 
 extern "C" int pcub_sc_deletion_build_table(int32_t n0, double pd, double* table, void* stream) {
-    if (n0 != 3 || !table || ((uintptr_t)table & 7u) || !(pd >= 0.0 && pd <= 1.0)) return PCUB_EINVAL;
-    hipLaunchKernelGGL(k_del_n03_table, dim3(kN03States * kN03Row / 256), dim3(256), 0, (hipStream_t)stream, pd,
-                       table);
+    if ((n0 != 2 && n0 != 3) || !table || ((uintptr_t)table & 7u) || !(pd >= 0.0 && pd <= 1.0)) return PCUB_EINVAL;
+    if (n0 == 2)
+        hipLaunchKernelGGL(k_del_n02_table, dim3(1), dim3(256), 0, (hipStream_t)stream, pd, table);
+    else
+        hipLaunchKernelGGL(k_del_n03_table, dim3(kN03States * kN03Row / 256), dim3(256), 0, (hipStream_t)stream, pd,
+                           table);
     const int rc = (int)hipGetLastError();
     if (rc == 0) tab_register(table, pd);
     return rc;

@@ -99,8 +99,14 @@ PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, i
     }
 }
 
-template <int N0, int TB>
-__global__ __launch_bounds__(kDelBlock) void k_sc_del_dense(DelArgs A) {
+// GT (n0 = 2): the table comes built (pcub_sc_deletion_build_table) and is copied into LDS, instead
+// of each workgroup building it: the build's registers (n02_table_entry) set the kernel's peak
+// (89 -> 79 VGPRs at 64 trellises: 6 waves a SIMD instead of 5)
+// waves a SIMD the register allocation must allow (the SGPR count, 97..112, caps it at 6)
+constexpr int dense_waves(int tb) { return tb <= 6 ? 6 : tb == 7 ? 4 : 3; }
+
+template <int N0, int TB, bool GT = false>
+__global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(DelArgs A) {
     constexpr int L = 1 << N0, T = 1 << TB, G = kDenseG, LV = T / G, CPB = kDenseCPB;
     constexpr int NW = T > 64 ? T / 64 : 1;
     constexpr int WPC = (T * L + 31) / 32;
@@ -111,14 +117,18 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del_dense(DelArgs A) {
     __shared__ double tab2[N0 == 2 ? kN02States * kN02Row : 1];
     __shared__ uint32_t xs[CPB * WPC];
     extern __shared__ uint32_t rxb[];
-    const double* tab;  // n0 = 3: the caller's table, registered for this pd (sc_del.hip)
+    const double* tab;  // n0 = 3 (and n0 = 2 with GT): the caller's table, registered for this pd (sc_del.hip)
     if constexpr (N0 == 2) {
         // once per workgroup (persistent launch)
-        for (int i = threadIdx.x; i < kN02States * 5; i += kDelBlock)
-            n02_table_entry(i / 5, i % 5, A.pd, tab2 + (i / 5) * kN02Row);
+        if constexpr (GT) {
+            for (int i = threadIdx.x; i < kN02States * kN02Row; i += kDelBlock) tab2[i] = A.tab[i];
+        } else {
+            for (int i = threadIdx.x; i < kN02States * 5; i += kDelBlock)
+                n02_table_entry(i / 5, i % 5, A.pd, tab2 + (i / 5) * kN02Row);
+        }
         tab = tab2;
     } else {
-        tab = A.tab3;
+        tab = A.tab;
     }
     const int lane = threadIdx.x & 63;
     const int j = threadIdx.x & (G - 1);
@@ -216,6 +226,7 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del_dense(DelArgs A) {
     }
 }
 
-DelKern del_kernel_dense(int n0, int tb);  // sc_del_dense.hip; nullptr outside n0 2, 3 and tb 4 .. 8
+// sc_del_dense.hip; nullptr outside n0 2, 3 and tb 4 .. 8 (gt: n0 = 2 with a built table)
+DelKern del_kernel_dense(int n0, int tb, bool gt = false);
 
 }  // namespace pcub

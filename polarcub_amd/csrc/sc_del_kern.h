@@ -59,7 +59,7 @@ struct DelArgs {
     const uint32_t* fval_cw;  // [ceil(N/32)][B] per-codeword frozen values (export mode), or null
     double* leaf;           // [N][B] compact normalised leaves (export mode)
     int rw;                 // > 0: words per codeword of the bit-packed received words in LDS
-    const double* tab3;     // n0 = 3 without ones: the segment-state table (n03_table_entry), or null
+    const double* tab;      // n0 = 2, 3 without ones: the segment-state table (pcub_sc_deletion_build_table), or null
 };
 
 // XSub (sc_bin_body.h) for the export mode: no rate-0 node is skipped and the two
@@ -662,11 +662,11 @@ __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint3
     } else if constexpr (N0 == 3 && OC == 0) {
         // the segment-state table, when one was built for this pd (its stamp: entry 255 of state 0);
         // a wave-uniform branch, the stamp is one scalar load
-        if (A.tab3 && __double_as_longlong(A.tab3[kN03Row - 1]) == __double_as_longlong(A.pd)) {
+        if (A.tab && __double_as_longlong(A.tab[kN03Row - 1]) == __double_as_longlong(A.pd)) {
             uint32_t y = 0;
             if (m <= 8)
                 for (int i = 0; i < m; ++i) y |= (uint32_t)(bit(s + i) & 1) << i;
-            x = del_n03_tab(A.tab3 + (long long)n03_state(m, y) * kN03Row, cx);
+            x = del_n03_tab(A.tab + (long long)n03_state(m, y) * kN03Row, cx);
         } else {
             x = DelBase<L, T, EXP>::run(base_segment<L>(bit, s, m, A.pd), cx);
         }

@@ -166,8 +166,8 @@ def test_n03_table_paths_agree(sc, n):
 
 @pytest.mark.parametrize("n0,n", [(2, 6), (2, 8), (2, 9), (2, 10), (3, 7), (3, 9), (3, 10), (3, 11)])
 def test_dense_layout_matches_lane_layout(sc, n0, n):
-    """The table-driven layout (16 lanes a codeword, sc_del_dense.h) and k_sc_del's lane-per-trellis
-    layout decode identically (a ragged batch: padding codewords in the last workgroup), and
+    """The table-driven layout (16 lanes a codeword, sc_del_dense.h; with and without a built table)
+    and k_sc_del's lane-per-trellis layout decode identically (a ragged batch: padding codewords in the last workgroup), and
     agree with the oracle on a sample."""
     N = 1 << n
     pd = 0.1
@@ -183,17 +183,22 @@ def test_dense_layout_matches_lane_layout(sc, n0, n):
     words += [[], [1], [0] * 5, [int(b) for b in rng.integers(0, 2, 2 * N)]]
     rxt, ln = sc.pad_words(words)
     code = sc.CodeSpec(N, frozen, fval, device="cuda")
-    d = sc.DeletionDecoder(code, n0, pd)
     outs = []
-    for dense in (True, False):
+    # table-driven with a built table, table-driven without one (n0 = 2 builds it per workgroup,
+    # n0 = 3 falls back to k_sc_del), and the lane layout
+    for dense, use_table in ((True, True), (True, False), (False, True)):
+        d = sc.DeletionDecoder(code, n0, pd, use_table=use_table)
         prev = sc.set_deletion_dense(dense)
         try:
+            if dense and use_table:
+                assert d.dense_layout(rxt.shape[1], rxt.device)
             info, xhat = d.decode(rxt, ln)
             torch.cuda.synchronize()
         finally:
             sc.set_deletion_dense(prev)
         outs.append((info.cpu().numpy(), xhat.cpu().numpy()))
-    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1])
     for i in list(range(0, len(words), 9)) + [len(words) - 3, len(words) - 1]:
         x_ref, i_ref = tro.decode_deletion(words[i], n, n0, pd, frozen, fval)
         assert list(outs[0][0][i]) == i_ref and list(outs[0][1][i]) == x_ref, i

@@ -103,7 +103,7 @@ PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, i
 // of each workgroup building it: the build's registers (n02_table_entry) set the kernel's peak
 // (89 -> 79 VGPRs at 64 trellises: 6 waves a SIMD instead of 5)
 // waves a SIMD the register allocation must allow (the SGPR count, 97..112, caps it at 6)
-constexpr int dense_waves(int tb) { return tb <= 6 ? 6 : tb == 7 ? 4 : 3; }
+constexpr int dense_waves(int tb) { return tb <= 6 ? 6 : tb == 7 ? 5 : 3; }
 
 template <int N0, int TB, bool GT = false>
 __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(DelArgs A) {

@@ -104,7 +104,11 @@ class Awgn:
         self.dec = sc.BinaryDecoder(self.code)
         # global codewords [rank*B, (rank+1)*B), Philox keyed by (seed, codeword index)
         self.offset = mc.rank_offset(rank, self.B)
-        self.info_w, self.xy = mc.philox_batch(self.code, a.seed, self.offset, self.B, mc.CHANNEL_AWGN, self.sigma2)
+        # the root rows in the kernel's tiles (a wave's codewords contiguous, pcub_sc_decode_bin_tiled) unless
+        # --no-tile ([N][B][2] rows, pcub_sc_decode_bin)
+        self.tile = 0 if a.no_tile else sc.bin_tile(n)
+        self.info_w, self.xy = mc.philox_batch(self.code, a.seed, self.offset, self.B, mc.CHANNEL_AWGN, self.sigma2,
+                                               tile=self.tile)
         self.rank = rank
         self.outs = (torch.empty((self.code.info_words, self.B), dtype=torch.int32, device=device),
                      None if a.no_xhat else torch.empty((self.code.n_words, self.B), dtype=torch.int32, device=device),
@@ -112,7 +116,18 @@ class Awgn:
         self.dec.workspace(self.B)
 
     def step(self):
-        self.dec.decode_native(self.xy, out=self.outs)
+        if self.tile:
+            self.dec.decode_tiled_native(self.xy, self.B, out=self.outs)
+        else:
+            self.dec.decode_native(self.xy, out=self.outs)
+
+    def rows(self, ncw):
+        """The first ncw codewords' rows, [ncw, N, 2] (the reference's layout)."""
+        if not self.tile:
+            return self.xy[:, :ncw, :].permute(1, 0, 2).contiguous()
+        T = self.tile
+        nt = (ncw + T - 1) // T
+        return self.xy[:nt].permute(0, 2, 1, 3).reshape(nt * T, self.N, 2)[:ncw].contiguous()
 
     def errors(self):
         d = sc.unpack(self.outs[0], self.K)
@@ -146,11 +161,13 @@ class Awgn:
             metric="decoded codewords/sec at N=%d BI-AWGN, batch=%d per GPU; FER match vs reference" % (self.N, self.B),
             dtype="f64",
             data="synthetic: uniform info bits, GPU polar encoder, BI-AWGN Eb/N0=%.1f dB pairs generated on device "
-                 "(Philox keyed by global codeword index)" % a.ebn0,
+                 "(Philox keyed by global codeword index)%s" % (
+                     a.ebn0, ", rows in %d-codeword tiles [B/%d][N][%d][2]" % (self.tile, self.tile, self.tile)
+                     if self.tile else ", rows [N][B][2]"),
             config={"workload": "binary SC decode N=%d K=%d BI-AWGN %.1f dB (BASELINE configs[%d])"
                                 % (self.N, self.K, a.ebn0, 1 if self.n == 10 else 2),
                     "N": self.N, "K": self.K, "batch_per_gpu": self.B, "ebn0_db": a.ebn0,
-                    "kernel_variant": self.variant, "max_blocks_per_cu": a.max_blocks,
+                    "kernel_variant": self.variant, "max_blocks_per_cu": a.max_blocks, "root_tile": self.tile,
                     "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
 
     def cpu_baseline(self, seconds=12.0):
@@ -161,7 +178,7 @@ class Awgn:
         from oracle import orc
         orc.lib()
         code, ncw = self.code, 4096
-        sample = self.xy[:, :ncw, :].permute(1, 0, 2).contiguous().cpu().numpy()
+        sample = self.rows(ncw).cpu().numpy()
         t0 = time.perf_counter()
         orc.decode_bin(sample[:64], code.frozen_mask, code.frozen_values)
         per_cw = (time.perf_counter() - t0) / 64
@@ -540,6 +557,7 @@ def build_parser():
     ap.add_argument("--master-port", type=int, default=0, help="rendezvous port when launching ranks (0 = free port)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-xhat", action="store_true")
+    ap.add_argument("--no-tile", action="store_true", help="awgn: root rows [N][B][2] instead of the kernel's tiles")
     ap.add_argument("--e2e-chunk", type=int, default=1 << 18,
                     help="codewords per chunk of the end-to-end Monte-Carlo line (generation overlaps decode)")
     ap.add_argument("--no-e2e", action="store_true",

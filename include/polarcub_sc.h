@@ -68,6 +68,16 @@ int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, const uint32_
                        const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
                        uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The same decode with the root rows in tiles of T codewords: xy [ceil(B/T)][N][T][2] f64, codeword b's
+ * row i at ((b / T) N + i) T + b % T (the last tile's padding columns are never read).  With T =
+ * pcub_sc_bin_tile(log2N) -- the codewords one wave of the kernel decodes -- each wave reads its
+ * codewords' rows as one contiguous block instead of 2N rows 16 B wide spread B * 16 bytes apart
+ * (N = 1024: 78 vs 75 M codewords/s).  T = 0 is the [N][B][2] layout of pcub_sc_decode_bin. */
+int pcub_sc_bin_tile(int32_t log2N);
+int pcub_sc_decode_bin_tiled(const double* xy, int64_t B, int32_t log2N, int32_t tile, const uint32_t* frozen_mask,
+                             const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
+                             uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream);
+
 /* q-ary SC decode (linear domain), 2 <= q <= 8, N >= 4.
  *   xy        [N][B][q] f64 joint probabilities P(X_i = x, Y_i = y_i)
  *   frozen    [N] u8 (1 = frozen; frozen symbols are 0, QaryPolarEncoderDecoder.py:351)
@@ -224,11 +234,20 @@ int pcub_leaf_marginals(const double* leaf, int64_t count, double* marginals, vo
 /* Binary SC decode of compact normalised rows: xc [N][B] f64, +r standing for the joint row
  * (1, r) and -r for (r, 1) (NaN: (0, 0)).  The same decode as pcub_sc_decode_bin on those pairs
  * (the reference's arithmetic on a row with a 1 in it is the compact one), from 8 bytes a position
- * instead of 16.  Workspace: pcub_sc_decode_bin_compact_workspace(B, log2N) bytes. */
+ * instead of 16.  Workspace: pcub_sc_decode_bin_compact_workspace(B, log2N) bytes.
+ * pcub_sc_decode_bin_compact_direct(log2N): 1 when that code length runs a compact-root kernel,
+ * 0 when the call expands the rows into pairs in its workspace first (B * N * 16 more bytes). */
+int pcub_sc_decode_bin_compact_direct(int32_t log2N);
 size_t pcub_sc_decode_bin_compact_workspace(int64_t B, int32_t log2N);
 int pcub_sc_decode_bin_compact(const double* xc, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
                                const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
                                uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream);
+/* ... with the rows in tiles of T codewords ([ceil(B/T)][N][T] f64; workspace for the padded batch:
+ * pcub_sc_decode_bin_compact_workspace(ceil(B/T) T, log2N)). */
+int pcub_sc_decode_bin_compact_tiled(const double* xc, int64_t B, int32_t log2N, int32_t tile,
+                                     const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K,
+                                     uint32_t* info_words, uint32_t* xhat_words, uint32_t* u_words, void* workspace,
+                                     size_t workspace_bytes, void* stream);
 
 /* Device Monte-Carlo (encodeDecodeSimulation, BinaryPolarEncoderDecoder.py:328-387, as a
  * batched pipeline).  Codeword g's draws come from Philox4x32-10 keyed by (seed, g), so
@@ -248,6 +267,11 @@ int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int
                     const uint32_t* x_words, double* xy, void* stream);
 int pcub_mc_channel_norm(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel, double param,
                          const uint32_t* x_words, double* out, int32_t compact, void* stream);
+/* the same rows written in tiles of T codewords (pcub_sc_decode_bin_tiled's layout; T = 0: [N][B]) */
+int pcub_mc_channel_tiled(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel, double param,
+                          const uint32_t* x_words, double* xy, int32_t tile, void* stream);
+int pcub_mc_channel_norm_tiled(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel, double param,
+                               const uint32_t* x_words, double* out, int32_t compact, int32_t tile, void* stream);
 int pcub_mc_count_errors(const uint32_t* decoded_words, const uint32_t* sent_words, int64_t B, int32_t K,
                          uint64_t* counters, void* stream);
 size_t pcub_mc_run_bin_workspace(int64_t chunk, int32_t log2N, int32_t K);

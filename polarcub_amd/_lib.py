@@ -127,11 +127,27 @@ def lib():
     L.pcub_mc_channel.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p, _c_void_p]
     L.pcub_mc_count_errors.restype = ctypes.c_int
     L.pcub_mc_count_errors.argtypes = [_c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p]
+    L.pcub_sc_bin_tile.restype = ctypes.c_int
+    L.pcub_sc_bin_tile.argtypes = [_i32]
+    L.pcub_sc_decode_bin_tiled.restype = ctypes.c_int
+    L.pcub_sc_decode_bin_tiled.argtypes = [_c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                                           _c_void_p, _c_void_p, ctypes.c_size_t, _c_void_p]
+    L.pcub_sc_decode_bin_compact_tiled.restype = ctypes.c_int
+    L.pcub_sc_decode_bin_compact_tiled.argtypes = [_c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p, _i32, _c_void_p,
+                                                   _c_void_p, _c_void_p, _c_void_p, ctypes.c_size_t, _c_void_p]
+    L.pcub_sc_decode_bin_compact_direct.restype = ctypes.c_int
+    L.pcub_sc_decode_bin_compact_direct.argtypes = [_i32]
     L.pcub_sc_decode_bin_compact_workspace.restype = ctypes.c_size_t
     L.pcub_sc_decode_bin_compact_workspace.argtypes = [_i64, _i32]
     L.pcub_sc_decode_bin_compact.restype = ctypes.c_int
     L.pcub_sc_decode_bin_compact.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                                              _c_void_p, _c_void_p, ctypes.c_size_t, _c_void_p]
+    L.pcub_mc_channel_tiled.restype = ctypes.c_int
+    L.pcub_mc_channel_tiled.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p, _i32,
+                                        _c_void_p]
+    L.pcub_mc_channel_norm_tiled.restype = ctypes.c_int
+    L.pcub_mc_channel_norm_tiled.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p,
+                                             _i32, _i32, _c_void_p]
     L.pcub_mc_channel_norm.restype = ctypes.c_int
     L.pcub_mc_channel_norm.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p, _i32,
                                        _c_void_p]
@@ -160,11 +176,12 @@ EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_b
            "pcub_sc_leaf_deletion_supported", "pcub_sc_decode_deletion", "pcub_sc_leaf_bin_workspace", "pcub_sc_leaf_bin", "pcub_sc_leaf_deletion",
            "pcub_sc_prior_bin_workspace", "pcub_sc_prior_bin",
            "pcub_sc_decode_qary_log_workspace", "pcub_sc_decode_qary_log",
-           "pcub_scl_qary_workspace", "pcub_scl_qary", "pcub_scl_qary_log", "pcub_leaf_marginals", "pcub_mc_info", "pcub_mc_channel", "pcub_mc_count_errors", "pcub_mc_channel_norm", "pcub_sc_decode_bin_compact_workspace",
+           "pcub_scl_qary_workspace", "pcub_scl_qary", "pcub_scl_qary_log", "pcub_leaf_marginals", "pcub_mc_info", "pcub_mc_channel", "pcub_mc_count_errors", "pcub_mc_channel_norm", "pcub_sc_decode_bin_compact_direct", "pcub_sc_decode_bin_compact_workspace",
            "pcub_sc_decode_bin_compact", "pcub_mc_info_qary", "pcub_mc_channel_qsc", "pcub_mc_deletion",
            "pcub_mc_run_bin_workspace", "pcub_mc_run_bin", "pcub_sc_deletion_table_bytes",
            "pcub_sc_deletion_build_table", "pcub_sc_decode_deletion_tab", "pcub_sc_leaf_deletion_tab",
-           "pcub_sc_set_deletion_dense", "pcub_sc_deletion_dense_layout"]
+           "pcub_sc_set_deletion_dense", "pcub_sc_deletion_dense_layout", "pcub_sc_bin_tile", "pcub_sc_decode_bin_tiled",
+           "pcub_sc_decode_bin_compact_tiled", "pcub_mc_channel_tiled", "pcub_mc_channel_norm_tiled"]
 
 
 def check(rc, what):

@@ -41,7 +41,8 @@ KernFn variant_kernel(int v) {
     if (KernFn k = bin_kernel_part2(v)) return k;
     if (KernFn k = bin_kernel_part3(v)) return k;
     if (KernFn k = bin_kernel_part4(v)) return k;
-    return bin_kernel_part5(v);
+    if (KernFn k = bin_kernel_part5(v)) return k;
+    return bin_kernel_part6(v);
 }
 
 // {32, 4, 2, NT, re-encoded bits in LDS, split last level, prefetch 2}: at N=1024 one stored
@@ -183,10 +184,10 @@ extern "C" size_t pcub_sc_decode_bin_workspace(int64_t B, int32_t log2N) {
 namespace {
 
 // raw pairs xy, or compact rows xc through a variant's compact-root twin (the caller checks one exists)
-int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
-                    const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
-                    uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream) {
-    if (B < 0 || log2N < 0 || log2N > 24 || !frozen_mask || !frozen_val) return PCUB_EINVAL;
+int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N, int32_t tile,
+                    const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K, uint32_t* info_words,
+                    uint32_t* xhat_words, uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream) {
+    if (B < 0 || log2N < 0 || log2N > 24 || tile < 0 || tile > 4096 || !frozen_mask || !frozen_val) return PCUB_EINVAL;
     if (K < 0 || K > (1 << log2N) || (K > 0 && !info_words) || (B > 0 && !xy && !xc)) return PCUB_EINVAL;
     if (B == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
@@ -204,6 +205,7 @@ int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N
     A.ybits = nullptr;
     A.nslots = 0;
     A.ef = nullptr;
+    A.tile = tile;
     if (log2N <= 5) {
         const dim3 grid((unsigned)((B + kBlock - 1) / kBlock));
         switch (log2N) {
@@ -241,17 +243,18 @@ int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N
     return (int)hipGetLastError();
 }
 
-// compact normalised rows -> (1, r) / (r, 1) pairs; NaN -> (0, 0)
+// compact normalised rows -> (1, r) / (r, 1) pairs; NaN -> (0, 0).  Grid-stride over a capped grid:
+// B * N reaches past 2^32 work items (a 1-D dispatch's limit) at N >= 2^14 with 2^18-codeword chunks.
 __global__ __launch_bounds__(kBlock) void k_expand_compact(const double* xc, long long count, double2* xy) {
-    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= count) return;
-    const double v = xc[i];
-    const double r = __builtin_fabs(v);
-    double2 o;
-    if (v != v) o = double2{0.0, 0.0};
-    else if (__builtin_signbit(v)) o = double2{r, 1.0};
-    else o = double2{1.0, r};
-    xy[i] = o;
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < count; i += (long long)gridDim.x * kBlock) {
+        const double v = xc[i];
+        const double r = __builtin_fabs(v);
+        double2 o;
+        if (v != v) o = double2{0.0, 0.0};
+        else if (__builtin_signbit(v)) o = double2{r, 1.0};
+        else o = double2{1.0, r};
+        xy[i] = o;
+    }
 }
 
 // the compact path runs a compact-root kernel when the variant picked for 2^n has one (and the
@@ -264,8 +267,30 @@ extern "C" int pcub_sc_decode_bin(const double* xy, int64_t B, int32_t log2N, co
                                   const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
                                   uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream) {
     if (!xy && B > 0) return PCUB_EINVAL;
-    return decode_bin_impl(xy, nullptr, B, log2N, frozen_mask, frozen_val, K, info_words, xhat_words, u_words,
+    return decode_bin_impl(xy, nullptr, B, log2N, 0, frozen_mask, frozen_val, K, info_words, xhat_words, u_words,
                            workspace, workspace_bytes, stream);
+}
+
+// the codewords one wave of the kernel that runs at 2^log2N decodes (64 / lanes per codeword): the
+// tile width whose root rows a wave reads as one contiguous block
+extern "C" int pcub_sc_bin_tile(int32_t log2N) {
+    if (log2N < 0 || log2N > 24) return PCUB_EINVAL;
+    if (log2N <= 5) return 64;
+    return 64 / kVar[pick_variant(log2N)].G;
+}
+
+extern "C" int pcub_sc_decode_bin_tiled(const double* xy, int64_t B, int32_t log2N, int32_t tile,
+                                        const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K,
+                                        uint32_t* info_words, uint32_t* xhat_words, uint32_t* u_words, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+    if (!xy && B > 0) return PCUB_EINVAL;
+    return decode_bin_impl(xy, nullptr, B, log2N, tile, frozen_mask, frozen_val, K, info_words, xhat_words, u_words,
+                           workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcub_sc_decode_bin_compact_direct(int32_t log2N) {
+    if (log2N < 0 || log2N > 24) return PCUB_EINVAL;
+    return compact_direct(log2N) ? 1 : 0;
 }
 
 extern "C" size_t pcub_sc_decode_bin_compact_workspace(int64_t B, int32_t log2N) {
@@ -275,24 +300,48 @@ extern "C" size_t pcub_sc_decode_bin_compact_workspace(int64_t B, int32_t log2N)
     return ((w + 255) & ~(size_t)255) + (size_t)B * ((size_t)1 << log2N) * sizeof(double2);
 }
 
-extern "C" int pcub_sc_decode_bin_compact(const double* xc, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
-                                          const uint32_t* frozen_val, int32_t K, uint32_t* info_words,
-                                          uint32_t* xhat_words, uint32_t* u_words, void* workspace,
-                                          size_t workspace_bytes, void* stream) {
+namespace {
+
+int decode_compact(const double* xc, int64_t B, int32_t log2N, int32_t tile, const uint32_t* frozen_mask,
+                   const uint32_t* frozen_val, int32_t K, uint32_t* info_words, uint32_t* xhat_words,
+                   uint32_t* u_words, void* workspace, size_t workspace_bytes, void* stream) {
     if (B < 0 || log2N < 0 || log2N > 24) return PCUB_EINVAL;
     if (B == 0) return 0;
     if (!xc || !workspace) return PCUB_EINVAL;
     if (compact_direct(log2N))
-        return decode_bin_impl(nullptr, xc, B, log2N, frozen_mask, frozen_val, K, info_words, xhat_words, u_words,
-                               workspace, workspace_bytes, stream);
+        return decode_bin_impl(nullptr, xc, B, log2N, tile, frozen_mask, frozen_val, K, info_words, xhat_words,
+                               u_words, workspace, workspace_bytes, stream);
     const size_t w = pcub_sc_decode_bin_workspace(B, log2N);
     const size_t off = (w + 255) & ~(size_t)255;
-    const long long count = B * (1LL << log2N);
+    // element-wise: the pairs keep the rows' layout; a tiled layout spans whole tiles (the caller
+    // sizes the workspace for the padded batch, pcub_sc_decode_bin_compact_workspace(ceil(B/T) T, n))
+    const long long Bp = tile > 0 ? (B + tile - 1) / tile * tile : B;
+    const long long count = Bp * (1LL << log2N);
     if (workspace_bytes < off + (size_t)count * sizeof(double2)) return PCUB_EINVAL;
     double2* xy = (double2*)((char*)workspace + off);
-    hipLaunchKernelGGL(k_expand_compact, dim3((unsigned)((count + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+    const long long eb = (count + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_expand_compact, dim3((unsigned)(eb < 65536 ? eb : 65536)), dim3(kBlock), 0,
                        (hipStream_t)stream, xc, count, xy);
     if (hipGetLastError() != hipSuccess) return (int)hipErrorLaunchFailure;
-    return decode_bin_impl((const double*)xy, nullptr, B, log2N, frozen_mask, frozen_val, K, info_words, xhat_words,
-                           u_words, workspace, w, stream);
+    return decode_bin_impl((const double*)xy, nullptr, B, log2N, tile, frozen_mask, frozen_val, K, info_words,
+                           xhat_words, u_words, workspace, w, stream);
+}
+
+}  // namespace
+
+extern "C" int pcub_sc_decode_bin_compact(const double* xc, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
+                                          const uint32_t* frozen_val, int32_t K, uint32_t* info_words,
+                                          uint32_t* xhat_words, uint32_t* u_words, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+    return decode_compact(xc, B, log2N, 0, frozen_mask, frozen_val, K, info_words, xhat_words, u_words, workspace,
+                          workspace_bytes, stream);
+}
+
+extern "C" int pcub_sc_decode_bin_compact_tiled(const double* xc, int64_t B, int32_t log2N, int32_t tile,
+                                                const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K,
+                                                uint32_t* info_words, uint32_t* xhat_words, uint32_t* u_words,
+                                                void* workspace, size_t workspace_bytes, void* stream) {
+    if (tile < 0 || tile > 4096) return PCUB_EINVAL;
+    return decode_compact(xc, B, log2N, tile, frozen_mask, frozen_val, K, info_words, xhat_words, u_words, workspace,
+                          workspace_bytes, stream);
 }

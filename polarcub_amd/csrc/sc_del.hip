@@ -26,57 +26,64 @@ constexpr int kMaxOnes = 3;
 
 std::atomic<int> g_dense{1};  // the table-driven layout allowed (pcub_sc_set_deletion_dense)
 
-// n0 = 3 tables built by pcub_sc_deletion_build_table in this process, with their pd: the
-// table-driven kernel reads a table without checking its stamp, so it runs only on a (table, pd)
-// pair registered here; any other table goes to k_sc_del, which checks the stamp per launch.
-std::mutex g_tab_mu;
-std::vector<std::pair<const double*, uint64_t>> g_tabs;
+// Status words of table-checked launches (one ring per device; sc_del_kern.h, DelArgs::gate): a
+// table-driven launch that rejects its table writes its launch id into its word, and the gated
+// fallback launch behind it on the same stream decodes the batch without the table only then.
+// Ids are unique per process, so a word left by an earlier launch never matches.
+constexpr int kGateRing = 1024;
+constexpr int kMaxDevices = 64;
+std::mutex g_gate_mu;
+unsigned long long* g_gate_ring[kMaxDevices] = {};
+std::atomic<unsigned long long> g_gate_next{1};
 
-uint64_t pd_bits(double pd) {
-    uint64_t b;
-    std::memcpy(&b, &pd, sizeof b);
-    return b;
+int gate_slot(unsigned long long** slot, unsigned long long* id) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    if (dev < 0 || dev >= kMaxDevices) return (int)hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_gate_mu);
+    if (!g_gate_ring[dev]) {
+        void* p = nullptr;
+        if ((e = hipMalloc(&p, kGateRing * sizeof(unsigned long long))) != hipSuccess) return (int)e;
+        if ((e = hipMemset(p, 0, kGateRing * sizeof(unsigned long long))) != hipSuccess) return (int)e;
+        g_gate_ring[dev] = (unsigned long long*)p;
+    }
+    *id = g_gate_next.fetch_add(1);
+    *slot = g_gate_ring[dev] + (*id % kGateRing);
+    return 0;
 }
 
-bool tab_registered(const double* t, double pd) {
-    if (!t) return false;
-    std::lock_guard<std::mutex> lk(g_tab_mu);
-    for (const auto& e : g_tabs)
-        if (e.first == t) return e.second == pd_bits(pd);
-    return false;
+// the table header (sc_del_kern.h, tab_ok): magic, n0, pd, zeros
+__device__ void tab_header(double* tab, int n0, double pd) {
+    tab[0] = from_bits((long long)kTabMagic);
+    tab[1] = (double)n0;
+    tab[2] = pd;
+    for (int i = 3; i < kTabHdr; ++i) tab[i] = 0.0;
 }
 
-void tab_register(const double* t, double pd) {
-    std::lock_guard<std::mutex> lk(g_tab_mu);
-    for (auto& e : g_tabs)
-        if (e.first == t) {
-            e.second = pd_bits(pd);
-            return;
-        }
-    if (g_tabs.size() >= 64) g_tabs.erase(g_tabs.begin());  // bounded: the oldest falls back to k_sc_del
-    g_tabs.emplace_back(t, pd_bits(pd));
-}
-
-// the n0 = 3 segment-state table: one thread per entry, 512 x 256 doubles (entry j of a row: value
-// k = floor(log2(j + 1)) after history j + 1 - 2^k; entry 255: pd)
+// the n0 = 3 segment-state table: one thread per entry, the header then 512 x 256 doubles (entry j
+// of a row: value k = floor(log2(j + 1)) after history j + 1 - 2^k; entry 255: padding)
 __global__ __launch_bounds__(256) void k_del_n03_table(double pd, double* tab) {
     const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) tab_header(tab, 3, pd);
     if (i >= kN03States * kN03Row) return;
     const int st = i / kN03Row, j = i % kN03Row;
     if (j == kN03Row - 1) {
-        tab[i] = pd;
+        tab[kTabHdr + i] = 0.0;
         return;
     }
     int k = 0;
     while ((2 << k) <= j + 1) ++k;
-    tab[i] = n03_table_entry(st, k, (uint32_t)(j + 1 - (1 << k)), pd);
+    tab[kTabHdr + i] = n03_table_entry(st, k, (uint32_t)(j + 1 - (1 << k)), pd);
 }
 
-// the n0 = 2 table (trellis_n02.h): one thread per (state, child) row part, entry 15 of every row pd
+// the n0 = 2 table (trellis_n02.h): the header, then one thread per (state, child) row part (entry 15
+// of every row padding)
 __global__ __launch_bounds__(256) void k_del_n02_table(double pd, double* tab) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < kN02States * 5) n02_table_entry(i / 5, i % 5, pd, tab + (i / 5) * kN02Row);
-    if (i < kN02States) tab[i * kN02Row + kN02Row - 1] = pd;
+    if (i == 0) tab_header(tab, 2, pd);
+    if (i < kN02States * 5) n02_table_entry(i / 5, i % 5, pd, tab + kTabHdr + (i / 5) * kN02Row);
+    if (i < kN02States) tab[kTabHdr + i * kN02Row + kN02Row - 1] = 0.0;
 }
 
 DelKern del_kernel(int n0, int tb, bool exp, int ones) {
@@ -109,14 +116,28 @@ OnesProbs ones_probs(int ones, double pd) {
     return op;
 }
 
-// the table-driven layout (sc_del_dense.h) when the stage has a table: n0 = 2 (built per
-// workgroup) or n0 = 3 with a table this library built for pd, no ones, 16 .. 256 trellises,
-// and the group's received words fit LDS bit-packed
-bool use_dense(int n, int n0, int ones, int stride, const double* table, double pd) {
+// the table-driven layout (sc_del_dense.h) when the stage has a table: n0 = 2 (the caller's, or
+// built per workgroup) or n0 = 3 with a table given (checked on the device: tab_ok), no ones,
+// 16 .. 256 trellises, and the group's received words fit LDS bit-packed
+bool use_dense(int n, int n0, int ones, int stride, const double* table) {
     const long long rw = ((long long)stride + 31) / 32;
-    return g_dense.load(std::memory_order_relaxed) && ones == 0 &&
-           (n0 == 2 || (n0 == 3 && tab_registered(table, pd))) && n - n0 >= 4 &&
-           (long long)kDenseCPB * rw * 4 <= kDenseMaxRxLds && del_kernel_dense(n0, n - n0) != nullptr;
+    return g_dense.load(std::memory_order_relaxed) && ones == 0 && (n0 == 2 || (n0 == 3 && table)) &&
+           n - n0 >= 4 && (long long)kDenseCPB * rw * 4 <= kDenseMaxRxLds && del_kernel_dense(n0, n - n0) != nullptr;
+}
+
+// A persistent grid for kernel k: one resident grid striding over the codeword groups.  The occupancy
+// API reports one workgroup a CU too many for 256-thread blocks at 97 .. 112 SGPRs
+// (MI355X_MICROARCH.md, occupancy row): 800 / (112 + 16) = 6 waves a SIMD at most, and an over-size
+// persistent grid leaves its last workgroups to run after the others.
+long long resident_grid(DelKern k, size_t lds, long long grid) {
+    int dev = 0, cus = 0, occ = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kDelBlock, lds) == hipSuccess && cus > 0 && occ > 0) {
+        const long long res = (long long)cus * (occ < 6 ? occ : 6);
+        if (grid > res) grid = res;
+    }
+    return grid;
 }
 
 int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, int32_t stride, int32_t n, int32_t n0,
@@ -145,37 +166,43 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     A.xhat = xhat_words;
     A.leaf = leaf;
     A.tab = ((n0 == 2 || n0 == 3) && ones == 0) ? table : nullptr;
-    DelKern k = kern;
-    long long cpb = kDelBlock >> (n - n0);
+    A.gate = nullptr;
+    A.gate_id = 0;
     const long long rw = ((long long)stride + 31) / 32;
-    const bool dense = !exp && use_dense(n, n0, ones, stride, table, pd);
-    if (dense) {
-        k = del_kernel_dense(n0, n - n0, n0 == 2 && tab_registered(table, pd));
-        cpb = kDenseCPB;
+    const bool dense = !exp && use_dense(n, n0, ones, stride, table);
+    // the table-driven kernel checks the caller's table on the device (n0 = 3, and n0 = 2 with a table
+    // given); behind it on the stream goes a gated fallback that decodes only if the check failed:
+    // for n0 = 2 the table-driven kernel that builds its own table, for n0 = 3 k_sc_del without one
+    const bool checked = dense && A.tab;
+    if (checked) {
+        const int rc = gate_slot(&A.gate, &A.gate_id);
+        if (rc) return rc;
     }
+    DelKern k = dense ? del_kernel_dense(n0, n - n0, n0 == 2 && A.tab) : kern;
+    long long cpb = dense ? kDenseCPB : kDelBlock >> (n - n0);
     long long grid = (B + cpb - 1) / cpb;
     // bit-packed received words in LDS when the group's words fit in 32 KiB (always for
     // the 64-trellis shapes; very long padded rows of small codes parse from HBM)
     A.rw = (dense || cpb * rw * 4 <= 32768) ? (int)rw : 0;
     const size_t lds = A.rw ? (size_t)(cpb * rw * 4) : 0;
-    // n0 = 2 without ones (and the table-driven layout): each workgroup first builds the
-    // segment-state table, so the launch is persistent (one resident grid striding over the
-    // codeword groups)
-    if (dense || (n0 == 2 && ones == 0)) {
-        int dev = 0, cus = 0, occ = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kDelBlock, lds) == hipSuccess && cus > 0 &&
-            occ > 0) {
-            // the occupancy API reports one workgroup a CU too many for 256-thread blocks at 97 .. 112
-            // SGPRs (MI355X_MICROARCH.md, occupancy row): 800 / (112 + 16) = 6 waves a SIMD at most,
-            // and an over-size persistent grid leaves its last workgroups to run after the others
-            const long long res = (long long)cus * (occ < 6 ? occ : 6);
-            if (grid > res) grid = res;
-        }
-    }
+    // n0 = 2 without ones (and the table-driven layout): each workgroup first builds or copies the
+    // segment-state table, so the launch is persistent
+    if (dense || (n0 == 2 && ones == 0)) grid = resident_grid(k, lds, grid);
     if (grid * kDelBlock > 0xffffffffLL) return PCUB_EINVAL;  // 32-bit dispatch grid (work-items)
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kDelBlock), lds, (hipStream_t)stream, A);
+    int rc = (int)hipGetLastError();
+    if (rc || !checked) return rc;
+    // the gated fallback: the same batch without the table, on a resident grid (its workgroups read
+    // the status word and leave when the table-driven launch succeeded)
+    DelArgs F = A;
+    F.tab = nullptr;
+    const bool fb_dense = n0 == 2;
+    const DelKern fk = fb_dense ? del_kernel_dense(2, n - n0, false) : kern;
+    const long long fcpb = fb_dense ? kDenseCPB : kDelBlock >> (n - n0);
+    F.rw = (fb_dense || fcpb * rw * 4 <= 32768) ? (int)rw : 0;
+    const size_t flds = F.rw ? (size_t)(fcpb * rw * 4) : 0;
+    const long long fgrid = resident_grid(fk, flds, (B + fcpb - 1) / fcpb);
+    hipLaunchKernelGGL(fk, dim3((unsigned)fgrid), dim3(kDelBlock), flds, (hipStream_t)stream, F);
     return (int)hipGetLastError();
 }
 
@@ -231,12 +258,12 @@ extern "C" int pcub_sc_set_deletion_dense(int32_t on) {
 extern "C" int pcub_sc_deletion_dense_layout(int32_t n, int32_t n0, int32_t ones, int32_t stride, const double* table,
                                              double pd) {
     return del_kernel(n0, n - n0, false, ones) != nullptr && stride >= 0 && stride <= 32767 &&
-           use_dense(n, n0, ones, stride, table, pd);
+           use_dense(n, n0, ones, stride, table);
 }
 
 extern "C" int64_t pcub_sc_deletion_table_bytes(int32_t n0) {
-    if (n0 == 2) return (int64_t)kN02States * kN02Row * (int64_t)sizeof(double);
-    return n0 == 3 ? (int64_t)kN03States * kN03Row * (int64_t)sizeof(double) : 0;
+    if (n0 == 2) return (int64_t)(kTabHdr + kN02States * kN02Row) * (int64_t)sizeof(double);
+    return n0 == 3 ? (int64_t)(kTabHdr + kN03States * kN03Row) * (int64_t)sizeof(double) : 0;
 }
 
 extern "C" int pcub_sc_deletion_build_table(int32_t n0, double pd, double* table, void* stream) {
@@ -246,7 +273,5 @@ extern "C" int pcub_sc_deletion_build_table(int32_t n0, double pd, double* table
     else
         hipLaunchKernelGGL(k_del_n03_table, dim3(kN03States * kN03Row / 256), dim3(256), 0, (hipStream_t)stream, pd,
                            table);
-    const int rc = (int)hipGetLastError();
-    if (rc == 0) tab_register(table, pd);
-    return rc;
+    return (int)hipGetLastError();
 }

@@ -117,18 +117,28 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
     __shared__ double tab2[N0 == 2 ? kN02States * kN02Row : 1];
     __shared__ uint32_t xs[CPB * WPC];
     extern __shared__ uint32_t rxb[];
-    const double* tab;  // n0 = 3 (and n0 = 2 with GT): the caller's table, registered for this pd (sc_del.hip)
+    if (A.gate && !(N0 == 3 || GT) && *A.gate != A.gate_id) return;  // a gated fallback (sc_del.hip)
+    if constexpr (N0 == 3 || GT) {
+        // the caller's table, checked on the device (one scalar load a workgroup): a table built for
+        // another n0 or pd is never read; the launch marks its status word and the gated fallback
+        // launch behind it decodes the batch without the table (sc_del.hip)
+        if (!tab_ok(A.tab, N0, A.pd)) {
+            if (threadIdx.x == 0 && A.gate) *A.gate = A.gate_id;
+            return;
+        }
+    }
+    const double* tab;  // n0 = 3 (and n0 = 2 with GT): the caller's table, past its header
     if constexpr (N0 == 2) {
         // once per workgroup (persistent launch)
         if constexpr (GT) {
-            for (int i = threadIdx.x; i < kN02States * kN02Row; i += kDelBlock) tab2[i] = A.tab[i];
+            for (int i = threadIdx.x; i < kN02States * kN02Row; i += kDelBlock) tab2[i] = A.tab[kTabHdr + i];
         } else {
             for (int i = threadIdx.x; i < kN02States * 5; i += kDelBlock)
                 n02_table_entry(i / 5, i % 5, A.pd, tab2 + (i / 5) * kN02Row);
         }
         tab = tab2;
     } else {
-        tab = A.tab;
+        tab = A.tab + kTabHdr;
     }
     const int lane = threadIdx.x & 63;
     const int j = threadIdx.x & (G - 1);

@@ -60,7 +60,21 @@ struct DelArgs {
     double* leaf;           // [N][B] compact normalised leaves (export mode)
     int rw;                 // > 0: words per codeword of the bit-packed received words in LDS
     const double* tab;      // n0 = 2, 3 without ones: the segment-state table (pcub_sc_deletion_build_table), or null
+    unsigned long long* gate;     // null, or this launch's status word (a table the kernel rejected, sc_del.hip)
+    unsigned long long gate_id;   // the value that marks the status word: this launch's table was rejected
 };
+
+// Segment-state tables (n0 = 2 and 3, pcub_sc_deletion_build_table) start with a header that every
+// kernel checks before it reads an entry: a magic word, n0 and pd (bit patterns), then the rows.
+// A table built for another n0 or pd, or a buffer that holds no table, is never read as one (one
+// uniform scalar load per workgroup; the n0 = 2 and n0 = 3 layouts cannot alias: the header is at
+// the same place in both and records n0).
+constexpr int kTabHdr = 8;  // doubles before the first row
+constexpr unsigned long long kTabMagic = 0x7063756254616232ull;
+PCUB_HD bool tab_ok(const double* tab, int n0, double pd) {
+    return tab && (unsigned long long)as_bits(tab[0]) == kTabMagic && as_bits(tab[1]) == as_bits((double)n0) &&
+           as_bits(tab[2]) == as_bits(pd);
+}
 
 // XSub (sc_bin_body.h) for the export mode: no rate-0 node is skipped and the two
 // normalised leaves of every M = 2 node are written (by group position 0) at
@@ -431,7 +445,7 @@ struct DelBase {
 // per pd by pcub_sc_deletion_table, reused by every decode) replays DelBase / DelNode's walk with
 // the same functions in the same order, so its entries are the per-lane values bit for bit.
 constexpr int kN03States = 512;
-constexpr int kN03Row = 256;  // 255 values per state, then pd (the stamp the kernel checks)
+constexpr int kN03Row = 256;  // 255 values per state, one pad
 
 PCUB_HD int n03_state(int m, uint32_t y) { return (m >= 0 && m <= 8) ? (1 << m) - 1 + (int)y : kN03States - 1; }
 
@@ -660,13 +674,13 @@ __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint3
             for (int i = 0; i < m; ++i) y |= (uint32_t)(bit(s + i) & 1) << i;
         x = del_n02_tab(n02tab + n02_state(m, y) * kN02Row, cx);
     } else if constexpr (N0 == 3 && OC == 0) {
-        // the segment-state table, when one was built for this pd (its stamp: entry 255 of state 0);
-        // a wave-uniform branch, the stamp is one scalar load
-        if (A.tab && __double_as_longlong(A.tab[kN03Row - 1]) == __double_as_longlong(A.pd)) {
+        // the segment-state table, when one was built for this n0 and pd (its header, tab_ok);
+        // a wave-uniform branch, the header is a scalar load
+        if (tab_ok(A.tab, 3, A.pd)) {
             uint32_t y = 0;
             if (m <= 8)
                 for (int i = 0; i < m; ++i) y |= (uint32_t)(bit(s + i) & 1) << i;
-            x = del_n03_tab(A.tab + (long long)n03_state(m, y) * kN03Row, cx);
+            x = del_n03_tab(A.tab + kTabHdr + (long long)n03_state(m, y) * kN03Row, cx);
         } else {
             x = DelBase<L, T, EXP>::run(base_segment<L>(bit, s, m, A.pd), cx);
         }
@@ -698,6 +712,9 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
     constexpr bool TAB = N0 == 2 && OC == 0;  // the n0 = 2 stage through the state table
     __shared__ uint32_t xs[CPB * WPC];
     __shared__ double n02tab[TAB ? kN02States * kN02Row : 1];
+    // a gated launch (the fallback behind a table-driven launch, sc_del.hip) runs only when that
+    // launch rejected its table
+    if (A.gate && *A.gate != A.gate_id) return;
     if constexpr (TAB) {
         // once per workgroup (the launch is persistent: a workgroup strides over codeword groups)
         for (int i = threadIdx.x; i < kN02States * 5; i += kDelBlock)

@@ -68,7 +68,14 @@ struct McArgs {
     double sigma;      // BI-AWGN: sqrt(sigma^2)
     double inv2s2;     //          1 / (2 sigma^2)
     double dens;       //          0.5 / sqrt(2 pi sigma^2) (uniform prior x Gaussian density)
+    int tile;          // channel rows: 0 = [N][B]; T > 0 = [ceil(B/T)][N][T] (pcub_sc_decode_bin_tiled)
 };
+
+// element (row i, codeword b) of a batch of channel rows
+PCUB_HD long long row_at(const McArgs& A, long long i, long long b) {
+    if (A.tile <= 0) return i * A.B + b;
+    return (b / A.tile) * ((long long)A.tile << A.n) + i * A.tile + b % A.tile;
+}
 
 // K uniform information bits per codeword: word w of codeword g is Philox
 // output lane (w & 3) of counter (g, kStreamInfo, w >> 2).
@@ -138,8 +145,8 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_
             o0 = bsc_pair(A, xw & 1u, u0);
             o1 = bsc_pair(A, (xw >> 1) & 1u, u1);
         }
-        xy[i0 * A.B + b] = o0;
-        if (i0 + 1 < N) xy[(i0 + 1) * A.B + b] = o1;
+        xy[row_at(A, i0, b)] = o0;
+        if (i0 + 1 < N) xy[row_at(A, i0 + 1, b)] = o1;
     }
 }
 
@@ -160,12 +167,12 @@ __device__ __forceinline__ double bsc_norm(const McArgs& A, uint32_t xb, double 
     return norm_pack(o.x, o.y);
 }
 
-__device__ __forceinline__ void put_norm(double* out, long long i, long long B, long long b, double c, bool compact) {
+__device__ __forceinline__ void put_norm(double* out, long long at, double c, bool compact) {
     if (compact) {
-        out[i * B + b] = c;
+        out[at] = c;
     } else {
         const double r = __builtin_fabs(c);
-        ((double2*)out)[i * B + b] = __builtin_signbit(c) ? double2{r, 1.0} : double2{1.0, r};
+        ((double2*)out)[at] = __builtin_signbit(c) ? double2{r, 1.0} : double2{1.0, r};
     }
 }
 
@@ -193,8 +200,8 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel_norm(McArgs A, const ui
             c0 = bsc_norm(A, xw & 1u, u0);
             c1 = bsc_norm(A, (xw >> 1) & 1u, u1);
         }
-        put_norm(out, i0, A.B, b, c0, COMPACT);
-        if (i0 + 1 < N) put_norm(out, i0 + 1, A.B, b, c1, COMPACT);
+        put_norm(out, row_at(A, i0, b), c0, COMPACT);
+        if (i0 + 1 < N) put_norm(out, row_at(A, i0 + 1, b), c1, COMPACT);
     }
 }
 
@@ -299,19 +306,20 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_deletion(McArgs A, const int32_
 extern "C" int pcub_mc_info(uint64_t seed, int64_t offset, int64_t B, int32_t K, uint32_t* info_words, void* stream) {
     if (B < 0 || offset < 0 || K < 0 || (K > 0 && B > 0 && !info_words)) return PCUB_EINVAL;
     if (B == 0 || K == 0) return 0;
-    McArgs A{seed, offset, B, 0, K, 0, 0.0, 0.0, 0.0, 0.0};
+    McArgs A{seed, offset, B, 0, K, 0, 0.0, 0.0, 0.0, 0.0, 0};
     hipLaunchKernelGGL(k_mc_info, dim3(grid_of(B)), dim3(kMcBlock), 0, (hipStream_t)stream, A, info_words);
     return (int)hipGetLastError();
 }
 
-extern "C" int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel, double param,
-                               const uint32_t* x_words, double* xy, void* stream) {
+extern "C" int pcub_mc_channel_tiled(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel,
+                                     double param, const uint32_t* x_words, double* xy, int32_t tile, void* stream) {
     if (B < 0 || offset < 0 || log2N < 0 || log2N > 24 || (channel != 0 && channel != 1)) return PCUB_EINVAL;
+    if (tile < 0 || tile > 4096) return PCUB_EINVAL;
     if (channel == 0 && !(param > 0.0)) return PCUB_EINVAL;
     if (channel == 1 && !(param >= 0.0 && param <= 1.0)) return PCUB_EINVAL;
     if (B == 0) return 0;
     if (!x_words || !xy) return PCUB_EINVAL;
-    McArgs A{seed, offset, B, log2N, 0, channel, param, 0.0, 0.0, 0.0};
+    McArgs A{seed, offset, B, log2N, 0, channel, param, 0.0, 0.0, 0.0, tile};
     if (channel == 0) {
         A.sigma = sqrt(param);
         A.inv2s2 = 1.0 / (2.0 * param);
@@ -329,14 +337,21 @@ extern "C" int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t
     return (int)hipGetLastError();
 }
 
-extern "C" int pcub_mc_channel_norm(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel,
-                                    double param, const uint32_t* x_words, double* out, int32_t compact, void* stream) {
+extern "C" int pcub_mc_channel(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel, double param,
+                               const uint32_t* x_words, double* xy, void* stream) {
+    return pcub_mc_channel_tiled(seed, offset, B, log2N, channel, param, x_words, xy, 0, stream);
+}
+
+extern "C" int pcub_mc_channel_norm_tiled(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel,
+                                          double param, const uint32_t* x_words, double* out, int32_t compact,
+                                          int32_t tile, void* stream) {
     if (B < 0 || offset < 0 || log2N < 0 || log2N > 24 || (channel != 0 && channel != 1)) return PCUB_EINVAL;
+    if (tile < 0 || tile > 4096) return PCUB_EINVAL;
     if (channel == 0 && !(param > 0.0)) return PCUB_EINVAL;
     if (channel == 1 && !(param >= 0.0 && param <= 1.0)) return PCUB_EINVAL;
     if (B == 0) return 0;
     if (!x_words || !out) return PCUB_EINVAL;
-    McArgs A{seed, offset, B, log2N, 0, channel, param, 0.0, 0.0, 0.0};
+    McArgs A{seed, offset, B, log2N, 0, channel, param, 0.0, 0.0, 0.0, tile};
     if (channel == 0) {
         A.sigma = sqrt(param);
         A.inv2s2 = 1.0 / (2.0 * param);
@@ -356,11 +371,16 @@ extern "C" int pcub_mc_channel_norm(uint64_t seed, int64_t offset, int64_t B, in
     return (int)hipGetLastError();
 }
 
+extern "C" int pcub_mc_channel_norm(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t channel,
+                                    double param, const uint32_t* x_words, double* out, int32_t compact, void* stream) {
+    return pcub_mc_channel_norm_tiled(seed, offset, B, log2N, channel, param, x_words, out, compact, 0, stream);
+}
+
 extern "C" int pcub_mc_info_qary(uint64_t seed, int64_t offset, int64_t B, int32_t K, int32_t q, uint8_t* info,
                                  void* stream) {
     if (B < 0 || offset < 0 || K < 0 || q < 2 || q > 255 || (K > 0 && B > 0 && !info)) return PCUB_EINVAL;
     if (B == 0 || K == 0) return 0;
-    McArgs A{seed, offset, B, 0, K, 0, 0.0, 0.0, 0.0, 0.0};
+    McArgs A{seed, offset, B, 0, K, 0, 0.0, 0.0, 0.0, 0.0, 0};
     hipLaunchKernelGGL(k_mc_info_qary, dim3(grid_of(B)), dim3(kMcBlock), 0, (hipStream_t)stream, A, (int)q, info);
     return (int)hipGetLastError();
 }
@@ -371,7 +391,7 @@ extern "C" int pcub_mc_channel_qsc(uint64_t seed, int64_t offset, int64_t B, int
         return PCUB_EINVAL;
     if (B == 0) return 0;
     if (!x || !xy) return PCUB_EINVAL;
-    McArgs A{seed, offset, B, log2N, 0, 2, p, 0.0, 0.0, 0.0};
+    McArgs A{seed, offset, B, log2N, 0, 2, p, 0.0, 0.0, 0.0, 0};
     const long long gx = (B + kMcBlock - 1) / kMcBlock;
     long long gy = (16384 + gx - 1) / gx;
     if (gy > ((long long)1 << log2N)) gy = (long long)1 << log2N;
@@ -388,7 +408,7 @@ extern "C" int pcub_mc_deletion(uint64_t seed, int64_t offset, int64_t B, int32_
     if (B < 0 || offset < 0 || log2N < 0 || log2N > 24 || W < 0 || !(pd >= 0.0 && pd <= 1.0)) return PCUB_EINVAL;
     if (B == 0) return 0;
     if (!tmpl || !x_words || !rx || !rx_len) return PCUB_EINVAL;
-    McArgs A{seed, offset, B, log2N, 0, 3, pd, 0.0, 0.0, 0.0};
+    McArgs A{seed, offset, B, log2N, 0, 3, pd, 0.0, 0.0, 0.0, 0};
     hipLaunchKernelGGL(k_mc_deletion, dim3(grid_of(B)), dim3(kMcBlock), 0, (hipStream_t)stream, A, tmpl, (int)W,
                        x_words, rx, rx_len);
     return (int)hipGetLastError();
@@ -425,19 +445,32 @@ struct McLayout {
     size_t info[2], x, xy[2], dec, dws, total;
 };
 
+// the compact-root decode exists for the variant this code length runs (sc_bin.hip); otherwise the
+// pipeline generates normalised pair rows (16 bytes a position) for the pair decode instead of
+// letting the compact entry expand them into a second chunk-sized buffer
+bool mc_compact(int32_t log2N) { return pcub_sc_decode_bin_compact_direct(log2N) == 1; }
+
+// the generation writes the rows in the decode kernel's tiles (pcub_sc_bin_tile: one wave's codewords
+// contiguous), padded to whole tiles
+int mc_tile(int32_t log2N) { return pcub_sc_bin_tile(log2N); }
+
 McLayout mc_layout(int64_t chunk, int32_t log2N, int32_t K) {
     McLayout L;
     const size_t N = (size_t)1 << log2N;
+    const size_t row = mc_compact(log2N) ? 8 : 16;  // bytes a position: compact row or pair
+    const int T = mc_tile(log2N);
+    const size_t cp = (size_t)((chunk + T - 1) / T) * T;  // the chunk padded to whole tiles
     const size_t iw = (size_t)((K + 31) / 32 > 0 ? (K + 31) / 32 : 1);
     const size_t nw = (N + 31) / 32;
     L.info[0] = 0;
     L.info[1] = L.info[0] + align256(iw * chunk * 4);
     L.x = L.info[1] + align256(iw * chunk * 4);
     L.xy[0] = L.x + align256(nw * chunk * 4);
-    L.xy[1] = L.xy[0] + align256(N * chunk * 8);
-    L.dec = L.xy[1] + align256(N * chunk * 8);
+    L.xy[1] = L.xy[0] + align256(N * cp * row);
+    L.dec = L.xy[1] + align256(N * cp * row);
     L.dws = L.dec + align256(iw * chunk * 4);
-    L.total = L.dws + align256(pcub_sc_decode_bin_compact_workspace(chunk, log2N));
+    L.total = L.dws + align256(mc_compact(log2N) ? pcub_sc_decode_bin_compact_workspace(chunk, log2N)
+                                                 : pcub_sc_decode_bin_workspace(chunk, log2N));
     return L;
 }
 
@@ -467,8 +500,11 @@ extern "C" int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int
                                double param, const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K,
                                int64_t chunk, uint64_t* counters, void* workspace, size_t workspace_bytes, void* stream) {
     if (count < 0 || offset < 0 || chunk <= 0 || !counters || !frozen_mask || !frozen_val) return PCUB_EINVAL;
+    if (log2N < 0 || log2N > 20) return PCUB_EINVAL;
     const McLayout L = mc_layout(chunk, log2N, K);
     if (!workspace || workspace_bytes < L.total) return PCUB_EINVAL;
+    const bool compact = mc_compact(log2N);
+    const int T = mc_tile(log2N);
     char* ws = (char*)workspace;
     uint32_t* x = (uint32_t*)(ws + L.x);
     uint32_t* dec = (uint32_t*)(ws + L.dec);
@@ -502,8 +538,11 @@ extern "C" int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int
         if (gs != ms && i >= 2 && (r = (int)hipStreamWaitEvent(gs, freed[k], 0))) return r;
         if (K > 0 && (r = pcub_mc_info(seed, offset + c0, B, K, info, gs))) return r;
         if ((r = pcub_polar_encode_bin(info, B, log2N, frozen_mask, frozen_val, K, x, gs))) return r;
-        // normalised rows in compact form (8 bytes a position) into the compact-root decode
-        if ((r = pcub_mc_channel_norm(seed, offset + c0, B, log2N, channel, param, x, xy, 1, gs))) return r;
+        // normalised rows in compact form (8 bytes a position) into the compact-root decode, or as
+        // pairs where this code length has no compact-root kernel
+        if ((r = pcub_mc_channel_norm_tiled(seed, offset + c0, B, log2N, channel, param, x, xy, compact ? 1 : 0, T,
+                                            gs)))
+            return r;
         if (gs != ms && (r = (int)hipEventRecord(ready[k], gs))) return r;
         return 0;
     };
@@ -514,9 +553,13 @@ extern "C" int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int
         if (!rc && i + 1 < nchunk) rc = gen(i + 1);  // enqueued before this chunk's decode
         if (rc) break;
         if (gs != ms && (rc = (int)hipStreamWaitEvent(ms, ready[k], 0))) break;
-        if ((rc = pcub_sc_decode_bin_compact((const double*)(ws + L.xy[k]), B, log2N, frozen_mask, frozen_val, K,
-                                             dec, nullptr, nullptr, ws + L.dws, L.total - L.dws, ms)))
-            break;
+        if (compact)
+            rc = pcub_sc_decode_bin_compact_tiled((const double*)(ws + L.xy[k]), B, log2N, T, frozen_mask, frozen_val, K,
+                                                  dec, nullptr, nullptr, ws + L.dws, L.total - L.dws, ms);
+        else
+            rc = pcub_sc_decode_bin_tiled((const double*)(ws + L.xy[k]), B, log2N, T, frozen_mask, frozen_val, K, dec,
+                                          nullptr, nullptr, ws + L.dws, L.total - L.dws, ms);
+        if (rc) break;
         if ((rc = pcub_mc_count_errors(dec, (const uint32_t*)(ws + L.info[k]), B, K, counters, ms))) break;
         if (gs != ms && (rc = (int)hipEventRecord(freed[k], ms))) break;
     }

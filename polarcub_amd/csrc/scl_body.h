@@ -50,6 +50,14 @@
 
 #include "sc_common.h"
 
+// test instrumentation hooks (tests/emu/scl_emu.cpp counts slab traffic and frame-loop iterations)
+#ifndef PCUB_SCL_TOUCH
+#define PCUB_SCL_TOUCH(bytes)
+#endif
+#ifndef PCUB_SCL_FRAME
+#define PCUB_SCL_FRAME()
+#endif
+
 namespace pcub {
 
 struct SclArgs {
@@ -120,8 +128,14 @@ struct SclCtx {
     bool lg;         // log domain
     double actual_prob;
 
-    PCUB_HD double& C(long long e) { return cells[e * ns]; }
-    PCUB_HD uint8_t& Bt(long long e) { return bytes[e * ns]; }
+    PCUB_HD double& C(long long e) {
+        PCUB_SCL_TOUCH(8);
+        return cells[e * ns];
+    }
+    PCUB_HD uint8_t& Bt(long long e) {
+        PCUB_SCL_TOUCH(1);
+        return bytes[e * ns];
+    }
     // row element of path slot `slot` at depth d (depth 0: the channel input, shared)
     PCUB_HD double row(int d, int slot, int pos, int x) {
         if (d == 0) return A->xy[((long long)pos * A->B + cw) * Y.q + x];
@@ -654,6 +668,7 @@ PCUB_HD int scl_run(SclCtx& c) {
     int sp = 0, ret = 0;
     st[0] = SclFrame{0, 0, 0, 0, 1, 0};
     while (sp >= 0) {
+        PCUB_SCL_FRAME();
         SclFrame& f = st[sp];
         const int S = Y.N >> f.d, H = S / 2;
         if (f.phase == 0) {

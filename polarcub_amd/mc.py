@@ -128,18 +128,22 @@ def qsc_batch(code, B, p, generator, chunk=1 << 16):
 CHANNEL_AWGN, CHANNEL_BSC = 0, 1
 
 
-def philox_batch(code, seed, offset, B, channel, param):
-    """Information words [ceil(K/32), B] and channel pairs [N, B, 2] for global codewords
-    [offset, offset + B) (pcub_mc_info -> pcub_polar_encode_bin -> pcub_mc_channel)."""
+def philox_batch(code, seed, offset, B, channel, param, tile=0):
+    """Information words [ceil(K/32), B] and channel pairs for global codewords [offset, offset + B)
+    (pcub_mc_info -> pcub_polar_encode_bin -> pcub_mc_channel): [N, B, 2], or with tile = T > 0 the
+    tiled layout [ceil(B/T), N, T, 2] (BinaryDecoder.decode_tiled_native; padding columns zero)."""
     from . import _lib
     L = _lib.lib()
     dev = code.device
     info = torch.zeros((max(1, code.info_words), B), dtype=torch.int32, device=dev)
     _lib.check(L.pcub_mc_info(int(seed), int(offset), B, code.K, sc._p(info), sc._stream()), "pcub_mc_info")
     x = sc.encode_native(code, info)
-    xy = torch.empty((code.N, B, 2), dtype=torch.float64, device=dev)
-    _lib.check(L.pcub_mc_channel(int(seed), int(offset), B, code.n, int(channel), float(param), sc._p(x), sc._p(xy),
-                                 sc._stream()), "pcub_mc_channel")
+    if tile:
+        xy = torch.zeros(((B + tile - 1) // tile, code.N, tile, 2), dtype=torch.float64, device=dev)
+    else:
+        xy = torch.empty((code.N, B, 2), dtype=torch.float64, device=dev)
+    _lib.check(L.pcub_mc_channel_tiled(int(seed), int(offset), B, code.n, int(channel), float(param), sc._p(x),
+                                       sc._p(xy), int(tile), sc._stream()), "pcub_mc_channel_tiled")
     return info, xy
 
 

@@ -180,6 +180,23 @@ def variants():
     return out
 
 
+def bin_tile(n):
+    """Codewords one wave of the binary decode kernel at N = 2^n decodes (pcub_sc_bin_tile): the tile
+    width of the tiled root layout [ceil(B/T), N, T, 2] that BinaryDecoder.decode_tiled_native reads
+    as one contiguous block per wave."""
+    return int(_lib.lib().pcub_sc_bin_tile(int(n)))
+
+
+def tile_rows(native, T):
+    """[N, B, ...] rows (codeword-minor) -> the tiled layout [ceil(B/T), N, T, ...] (zero-padded)."""
+    N, B = native.shape[0], native.shape[1]
+    nt = (B + T - 1) // T
+    pad = nt * T - B
+    if pad:
+        native = torch.cat([native, native.new_zeros((N, pad) + tuple(native.shape[2:]))], dim=1)
+    return native.reshape((N, nt, T) + tuple(native.shape[2:])).transpose(0, 1).contiguous()
+
+
 class BinaryDecoder:
     """Batched SC decoder for one CodeSpec; owns its device workspace."""
 
@@ -214,6 +231,33 @@ class BinaryDecoder:
                                            _p(uo), _p(ws), ws.numel(), _stream())
         _lib.check(rc, "pcub_sc_decode_bin")
         return info, xh, uo
+
+    def decode_tiled_native(self, xy_t, B, want_xhat=True, out=None):
+        """xy_t: the tiled root layout [ceil(B/T), N, T, 2] float64 on device (codeword b at tile b // T,
+        column b % T; tile_rows), B codewords.  The same decode as decode_native on the untiled rows;
+        each wave reads its codewords' rows as one contiguous block.  Returns packed
+        (info_words, xhat_words|None, None)."""
+        c = self.code
+        if xy_t.dtype != torch.float64 or xy_t.dim() != 4 or xy_t.shape[1] != c.N or xy_t.shape[3] != 2:
+            raise ValueError("xy_t must be float64 [ceil(B/T), N, T, 2] with N=%d" % c.N)
+        if not xy_t.is_cuda:
+            raise ValueError("xy_t must be a device tensor")
+        T = xy_t.shape[2]
+        if xy_t.shape[0] != (B + T - 1) // T:
+            raise ValueError("xy_t holds %d tiles of %d codewords, B=%d needs %d" % (xy_t.shape[0], T, B,
+                                                                                     (B + T - 1) // T))
+        xy_t = xy_t.contiguous()
+        dev = xy_t.device
+        if out is None:
+            info = torch.empty((max(1, c.info_words), B), dtype=torch.int32, device=dev)
+            xh = torch.empty((c.n_words, B), dtype=torch.int32, device=dev) if want_xhat else None
+        else:
+            info, xh, _ = out
+        ws = self.workspace(B)
+        rc = _lib.lib().pcub_sc_decode_bin_tiled(_p(xy_t), B, c.n, T, _p(c.fmask_dev), _p(c.fval_dev), c.K, _p(info),
+                                                 _p(xh), None, _p(ws), ws.numel(), _stream())
+        _lib.check(rc, "pcub_sc_decode_bin_tiled")
+        return info, xh, None
 
     def decode_compact_native(self, xc, want_xhat=True, out=None):
         """xc: [N, B] float64 compact normalised rows on device (+r: (1, r), -r: (r, 1)), the same
@@ -611,9 +655,12 @@ def set_deletion_dense(on):
 class DeletionDecoder:
     """Batched SC decoder over the deletion channel (CollectionOfBinaryTrellises built from
     each received word with buildCollectionOfBinaryTrellises_uniformInput_deletion, with
-    `ones` guard-band ones) for one CodeSpec.  With use_table (the default) and n0 = 3, ones = 0
-    the decoder builds the segment-state table for pd once per device
-    (pcub_sc_deletion_build_table) and every decode reads it; decisions are identical without it."""
+    `ones` guard-band ones) for one CodeSpec.  With use_table (the default), n0 = 2 or 3 and
+    ones = 0 the decoder builds the segment-state table for (n0, pd) once per device
+    (pcub_sc_deletion_build_table) and every decode passes it; the kernels check its header
+    (magic, n0, pd) on the device and decode without it when it does not match.  Decisions are
+    identical without a table: n0 = 3 then rebuilds the trellis levels per lane, n0 = 2 builds
+    the table per workgroup."""
 
     def __init__(self, code, n0, pd, ones=0, use_table=True):
         self.code = code

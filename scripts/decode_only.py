@@ -14,6 +14,7 @@ ap.add_argument("--n", type=int, default=10)
 ap.add_argument("--batch", type=int, default=1 << 20)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--variant", type=int, default=None)
+ap.add_argument("--no-tile", action="store_true", help="root rows [N][B][2] instead of the kernel's tiles (bench.py)")
 a = ap.parse_args()
 N = 1 << a.n
 K = N // 2
@@ -25,9 +26,15 @@ dec = sc.BinaryDecoder(code)
 gen = torch.Generator(device="cuda")
 gen.manual_seed(1)
 xy, info = mc.awgn_batch(code, a.batch, s2, gen)
+T = 0 if a.no_tile else sc.bin_tile(a.n)
+if T:
+    xy = sc.tile_rows(xy, T)
 outs = (torch.empty((code.info_words, a.batch), dtype=torch.int32, device="cuda"),
         torch.empty((code.n_words, a.batch), dtype=torch.int32, device="cuda"), None)
 for _ in range(a.reps):
-    dec.decode_native(xy, out=outs)
+    if T:
+        dec.decode_tiled_native(xy, a.batch, out=outs)
+    else:
+        dec.decode_native(xy, out=outs)
 torch.cuda.synchronize()
 print("done")

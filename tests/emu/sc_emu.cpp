@@ -23,6 +23,7 @@ extern "C" int emu_decode_bin(const double* xy, long long B, int n, const uint32
     A.xhat = xhat;
     A.uout = uout;
     A.ef = nullptr;
+    A.tile = 0;
     if (n <= 5) {
         for (long long b = 0; b < B; ++b) {
             switch (n) {
@@ -71,6 +72,7 @@ extern "C" int emu_decode_bin_compact(const double* xc, long long B, int n, cons
     A.info = info;
     A.xhat = xhat;
     A.uout = nullptr;
+    A.tile = 0;
     const long long nslots = 4;
     std::vector<double2> scr((size_t)(N / 2 - SR) * nslots + 1);
     std::vector<uint32_t> yb((size_t)(N / 32 + 2) * nslots);

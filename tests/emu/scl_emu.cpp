@@ -5,11 +5,22 @@
 
 #include <vector>
 
+// slab traffic and frame-loop iterations of the last emu_scl call (emu_scl_counts)
+static long long g_touch_bytes = 0, g_frames = 0;
+#define PCUB_SCL_TOUCH(b) (g_touch_bytes += (b))
+#define PCUB_SCL_FRAME() (++g_frames)
 #include "scl_body.h"
+
+extern "C" void emu_scl_counts(long long* bytes, long long* frames) {
+    *bytes = g_touch_bytes;
+    *frames = g_frames;
+}
 
 extern "C" int emu_scl(const double* xy, long long B, int q, int n, int L, const uint8_t* frozen,
                        const uint8_t* fvals, int nF, const uint8_t* actual, int K, uint8_t* out_info,
                        double* out_prob, int* out_size, double* out_actual, int use_log) {
+    g_touch_bytes = 0;
+    g_frames = 0;
     pcub::SclLayout Y;
     Y.init(n, q, L, K);
     std::vector<double> cells((size_t)Y.ncells);

@@ -47,22 +47,28 @@ def test_invalid_arguments_are_rejected_without_touching_the_device():
     assert L.pcub_transpose_pairs(None, 4, 4, 9, None, None) == _lib.EINVAL
     assert L.pcub_sc_decode_bin_workspace(0, 10) == 0
     # segment-state tables: sizes, argument checks, and the layout query (host-only code paths)
-    assert L.pcub_sc_deletion_table_bytes(2) == 32 * 16 * 8
-    assert L.pcub_sc_deletion_table_bytes(3) == 512 * 256 * 8
+    assert L.pcub_sc_deletion_table_bytes(2) == (8 + 32 * 16) * 8  # header (magic, n0, pd) + rows
+    assert L.pcub_sc_deletion_table_bytes(3) == (8 + 512 * 256) * 8
     assert L.pcub_sc_deletion_table_bytes(1) == 0 and L.pcub_sc_deletion_table_bytes(4) == 0
     assert L.pcub_sc_deletion_build_table(1, 0.1, ctypes.c_void_p(4096), None) == _lib.EINVAL
     assert L.pcub_sc_deletion_build_table(3, 0.1, None, None) == _lib.EINVAL
     assert L.pcub_sc_deletion_build_table(3, 0.1, ctypes.c_void_p(4097), None) == _lib.EINVAL  # misaligned
     assert L.pcub_sc_deletion_build_table(3, 1.5, ctypes.c_void_p(4096), None) == _lib.EINVAL
     # n0 = 2 runs the table-driven layout from 16 trellises on (its table can be built per
-    # workgroup); n0 = 3 only with a table this library built for pd; never with ones or n0 = 1, 4
+    # workgroup); n0 = 3 only with a table given (checked on the device: a rejected table sends the
+    # batch to the gated fallback); never with ones or n0 = 1, 4
     assert L.pcub_sc_deletion_dense_layout(8, 2, 0, 800, None, 0.1) == 1
     assert L.pcub_sc_deletion_dense_layout(5, 2, 0, 100, None, 0.1) == 0   # 8 trellises
     assert L.pcub_sc_deletion_dense_layout(8, 2, 1, 800, None, 0.1) == 0   # guard-band ones
     assert L.pcub_sc_deletion_dense_layout(10, 3, 0, 3000, None, 0.1) == 0  # no table
-    assert L.pcub_sc_deletion_dense_layout(10, 3, 0, 3000, ctypes.c_void_p(4096), 0.1) == 0  # not built here
+    assert L.pcub_sc_deletion_dense_layout(10, 3, 0, 3000, ctypes.c_void_p(4096), 0.1) == 1  # header checked on device
     assert L.pcub_sc_deletion_dense_layout(12, 4, 0, 9000, None, 0.1) == 0
     assert L.pcub_sc_deletion_dense_layout(8, 2, 0, 30000, None, 0.1) == 0  # rows past the LDS budget
+    # the compact-root decode: a kernel of its own where the default variant has a twin (N = 1024,
+    # 4096), else an expansion into pairs (the Monte-Carlo pipeline then generates pairs itself)
+    assert L.pcub_sc_decode_bin_compact_direct(10) == 1 and L.pcub_sc_decode_bin_compact_direct(12) == 1
+    assert L.pcub_sc_decode_bin_compact_direct(14) == 0 and L.pcub_sc_decode_bin_compact_direct(5) == 0
+    assert L.pcub_sc_decode_bin_compact_direct(30) == _lib.EINVAL
 
 
 def test_oracle_and_emulator_build():

@@ -9,7 +9,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 BIN_SETS = ["bsc_n64", "awgn_n1024", "awgn_n4096", "awgn_n256_lowsnr"]
-NVAR = 33  # kernel variants (sc_bin_kern.h); 24-30 and 32 keep the re-encoded bits in LDS, 26-28 and 30-32 split their last level (LDS + registers)
+NVAR = 38  # kernel variants (sc_bin_kern.h); 24-30, 32-37 keep the re-encoded bits in LDS, 26-28, 30-37 split their last level (LDS + registers), 33-37 speculate the plus transforms
 
 
 def _xy(g):
@@ -116,3 +116,50 @@ def test_decode_then_reencode_roundtrip_large(sc):
     di, dx = sc.BinaryDecoder(code).decode(xy)
     assert torch.equal(di, info)
     assert torch.equal(dx, x)
+
+
+@pytest.mark.parametrize("variant", [0, 7, 17, 24, 26, 31])
+def test_tiled_root_layout(sc, variant):
+    """pcub_sc_decode_bin_tiled: the root rows in tiles of T codewords ([ceil(B/T), N, T, 2], the
+    kernel's own wave width and others, ragged last tiles) decode exactly as the [N, B, 2] rows, for
+    the short-code kernels too, and the compact rows' tiled entry likewise."""
+    from oracle import orc
+    sc.set_variant(variant)
+    rng = np.random.default_rng(100 + variant)
+    try:
+        for N, B in [(16, 77), (64, 300), (1024, 333), (4096, 70)]:
+            n = N.bit_length() - 1
+            frozen = (rng.random(N) < 0.5).astype(np.uint8)
+            fval = (rng.random(N) < 0.5).astype(np.uint8)
+            xy = rng.random((B, N, 2))
+            xy[rng.random((B, N)) < 0.05] = 0.0
+            code = sc.CodeSpec(N, frozen, fval)
+            dec = sc.BinaryDecoder(code)
+            native = torch.from_numpy(np.ascontiguousarray(xy.transpose(1, 0, 2))).cuda()
+            ref_i, ref_x, _ = dec.decode_native(native)
+            for T in sorted({sc.bin_tile(n), 1, 5, 64}):
+                ti, tx, _ = dec.decode_tiled_native(sc.tile_rows(native, T), B)
+                assert torch.equal(ti, ref_i) and torch.equal(tx, ref_x), (N, T)
+            ri, rx = orc.decode_bin(xy[:40], frozen, fval)
+            assert np.array_equal(sc.unpack(ref_i, code.K).cpu().numpy()[:40], ri)
+            # compact rows (normalised pairs' ratios with the orientation in the sign)
+            p0, p1 = xy[..., 0], xy[..., 1]
+            with np.errstate(invalid="ignore", divide="ignore"):
+                xc = np.where(p1 > p0, -(p0 / p1), p1 / p0)
+            xct = torch.from_numpy(np.ascontiguousarray(xc.T)).cuda()
+            ci, cx, _ = dec.decode_compact_native(xct)
+            T = sc.bin_tile(n)
+            tiled = sc.tile_rows(xct, T)
+            from polarcub_amd import _lib
+            L = _lib.lib()
+            nt = (B + T - 1) // T
+            ws = torch.empty(int(L.pcub_sc_decode_bin_compact_workspace(nt * T, n)), dtype=torch.uint8, device="cuda")
+            info = torch.empty_like(ci)
+            xh = torch.empty_like(cx)
+            rc = L.pcub_sc_decode_bin_compact_tiled(sc._p(tiled), B, n, T, sc._p(code.fmask_dev), sc._p(code.fval_dev),
+                                                    code.K, sc._p(info), sc._p(xh), None, sc._p(ws), ws.numel(),
+                                                    sc._stream())
+            assert rc == 0
+            assert torch.equal(info, ci) and torch.equal(xh, cx), N
+    finally:
+        sc.set_variant()

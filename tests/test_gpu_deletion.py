@@ -135,8 +135,9 @@ def test_facade_dispatch_and_mc_line():
 @pytest.mark.parametrize("n", [5, 10, 11])
 def test_n03_table_paths_agree(sc, n):
     """n0 = 3: the segment-state table (pcub_sc_deletion_build_table, the table-driven layout), the
-    per-lane trellis levels (no table) and a table built for another pd (not registered for this
-    pd: k_sc_del, whose stamp check ignores it) decode identically, and agree with the oracle."""
+    per-lane trellis levels (no table), a table built for another pd and an n0 = 2 table's buffer
+    (both rejected by the kernel's header check: the gated fallback decodes without them) decode
+    identically, and agree with the oracle."""
     n0, pd = 3, 0.1
     N = 1 << n
     rng = np.random.default_rng(31 + n)
@@ -148,13 +149,16 @@ def test_n03_table_paths_agree(sc, n):
     rxt, ln = sc.pad_words(words)
     code = sc.CodeSpec(N, frozen, fval, device="cuda")
     outs = []
-    for mode in ("table", "plain", "stale"):
+    for mode in ("table", "plain", "stale", "n02"):
         d = sc.DeletionDecoder(code, n0, pd, use_table=(mode != "plain"))
         if mode == "stale":
             d._tables[str(rxt.device)] = sc.DeletionDecoder(code, n0, 0.2).table(rxt.device)
+        if mode == "n02":  # an n0 = 2 table for this very pd: its header says n0 = 2
+            d._tables[str(rxt.device)] = sc.DeletionDecoder(
+                sc.CodeSpec(256, np.ones(256, np.uint8), np.zeros(256, np.uint8), device="cuda"), 2, pd).table(rxt.device)
         if mode == "table":
             tab = d.table(rxt.device).cpu().numpy()
-            assert tab.shape == (512 * 256,) and np.all(tab[255::256] == pd)
+            assert tab.shape == (8 + 512 * 256,) and tab[1] == 3.0 and tab[2] == pd
         info, xhat = d.decode(rxt, ln)
         outs.append((info.cpu().numpy(), xhat.cpu().numpy()))
     for o in outs[1:]:
@@ -162,6 +166,31 @@ def test_n03_table_paths_agree(sc, n):
     for i in list(range(0, len(words), 7)) + [len(words) - 1]:
         x_ref, i_ref = tro.decode_deletion(words[i], n, n0, pd, frozen, fval)
         assert list(outs[0][0][i]) == i_ref and list(outs[0][1][i]) == x_ref, i
+
+
+def test_n02_foreign_tables_rejected(sc):
+    """n0 = 2 given an n0 = 3 table (for this pd) or an n0 = 2 table for another pd: the header check
+    rejects both and the gated fallback (the table-driven kernel building its own table) decodes
+    exactly as the table-less path."""
+    n, n0, pd = 8, 2, 0.1
+    N = 1 << n
+    rng = np.random.default_rng(5)
+    prng = random.Random(5)
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    words = [tro.deletion_channel(tro.add_guard_bands([int(b) for b in rng.integers(0, 2, N)], n, n0, 0.1, 0), pd,
+                                  prng) for _ in range(300)]
+    rxt, ln = sc.pad_words(words)
+    code = sc.CodeSpec(N, frozen, fval, device="cuda")
+    ref = sc.DeletionDecoder(code, n0, pd, use_table=False).decode(rxt, ln)
+    for other in (sc.DeletionDecoder(sc.CodeSpec(1024, np.ones(1024, np.uint8), np.zeros(1024, np.uint8), device="cuda"),
+                                     3, pd), sc.DeletionDecoder(code, n0, 0.3)):
+        d = sc.DeletionDecoder(code, n0, pd)
+        d._tables[str(rxt.device)] = other.table(rxt.device)
+        assert d.dense_layout(rxt.shape[1], rxt.device)
+        info, xhat = d.decode(rxt, ln)
+        assert np.array_equal(info.cpu().numpy(), ref[0].cpu().numpy())
+        assert np.array_equal(xhat.cpu().numpy(), ref[1].cpu().numpy())
 
 
 @pytest.mark.parametrize("n0,n", [(2, 6), (2, 8), (2, 9), (2, 10), (3, 7), (3, 9), (3, 10), (3, 11)])

@@ -210,3 +210,44 @@ def test_gpu_ir_simulation_log_matches_reference(which, capsys):
     assert fe == r["frame_error_prob"] and rate == r["rate"]
     assert [p.name for p in prl] == r["prob_results"]
     assert capsys.readouterr().out.splitlines()[:2] == r["printed"].splitlines()[:2]
+
+
+def test_gpu_list_decoder_n4096_l32_capped(sc):
+    """The large shape the ABI advertises (N = 4096, q = 4, L = 32; about 4.3 MB of slab a slot) with
+    the workspace capped to one workgroup's slots, so every lane decodes two codewords in turn.
+    Round 3's timeout here was the batch, not a hang: the frame loop ends after 5,525 iterations a
+    codeword (bound 3 (2N - 1)) and touches 729 MB of slab (tests/emu/scl_emu.cpp, emu_scl_counts),
+    so 2^17 codewords are ~95 TB of slab traffic.  Codewords match their single decodes and the
+    oracle."""
+    import torch
+    from polarcub_amd import _lib
+    rng = np.random.default_rng(4096)
+    q, n, L, B = 4, 12, 32, 96
+    N = 1 << n
+    frozen = np.zeros(N, np.uint8)
+    frozen[rng.permutation(N)[: N // 2]] = 1
+    nF = int(frozen.sum())
+    p = 0.11
+    tab = np.full((q, q), p / (q - 1))
+    np.fill_diagonal(tab, 1 - p)
+    x = rng.integers(0, q, (B, N))
+    y = np.where(rng.random((B, N)) < p, (x + rng.integers(1, q, (B, N))) % q, x)
+    xy_h = tab[y] / q  # [B][N][q] joint rows of a QSC(0.11)
+    fv_h = np.zeros((B, nF), np.uint8)
+    dec = sc.QaryListDecoder(q, N, frozen, L)
+    one_block = int(_lib.lib().pcub_scl_qary_workspace(64, q, n, L, N - nF))  # 64 slots: a grid of one
+    xy = torch.from_numpy(np.ascontiguousarray(xy_h.transpose(1, 0, 2))).cuda()
+    fv = torch.from_numpy(np.ascontiguousarray(fv_h.T)).cuda()
+    info, prob, size, _ = dec.decode_native(xy, fv, max_workspace_bytes=one_block)
+    torch.cuda.synchronize()
+    assert dec._ws.numel() <= one_block + 64
+    idx = [0, 70]  # lane 0's first and lane 6's second codeword
+    info1, prob1, size1, _ = sc.QaryListDecoder(q, N, frozen, L).decode_native(xy[:, idx].contiguous(),
+                                                                               fv[:, idx].contiguous())
+    assert torch.equal(size[idx], size1)
+    assert torch.equal(info[:, :, idx], info1) and torch.equal(prob[:, idx], prob1)
+    for b in idx:
+        k, oinfo, oprob, _ = so.list_decode(q, frozen, L, xy_h[b], fv_h[b])
+        assert int(size[b]) == k
+        assert info[:k, :, b].cpu().numpy().tolist() == oinfo
+        assert np.array_equal(prob[:k, b].cpu().numpy(), np.array(oprob))

@@ -284,39 +284,36 @@ class Deletion:
                     "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
 
     def cpu_baseline(self, seconds=10.0):
-        """oracle/trellis_oracle.py (pure Python restatement) in one process per host core
-        (the GIL rules out threads), each on its own slice of a bounded sample."""
-        from concurrent.futures import ProcessPoolExecutor
-        import multiprocessing as mp
+        """oracle/trellis_oracle.c (the C restatement of the reference's trellis SC; ctypes releases the
+        GIL) on the host threads, each on its own slice of a bounded sample of the bench's own
+        received words, repeated to about `seconds` of wall time."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle import orc
+        orc.lib()
         cores, cdesc = host_cores()
-        ncw = min(self.B, 256 * cores)
+        ncw = min(self.B, 64 * cores)
         rx = self.rx[:ncw].cpu().numpy()
         ln = self.rx_len[:ncw].cpu().numpy()
-        words = [list(map(int, rx[i, :ln[i]])) for i in range(ncw)]
         fm, fv = self.code.frozen_mask, self.code.frozen_values
-        parts = [words[(i * ncw) // cores:((i + 1) * ncw) // cores] for i in range(cores)]
-        with ProcessPoolExecutor(cores, mp_context=mp.get_context("spawn")) as ex:
-            list(ex.map(_del_oracle_part, [(p[:1], self.n, self.n0, self.pd, fm, fv, 0.0) for p in parts]))  # warm
-            t0 = time.perf_counter()
-            done = sum(ex.map(_del_oracle_part, [(p, self.n, self.n0, self.pd, fm, fv, seconds) for p in parts]))
-            dt = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        orc.decode_deletion(rx[:8], ln[:8], self.n, self.n0, self.pd, fm, fv, self.ones)
+        per_cw = max((time.perf_counter() - t0) / 8, 1e-7)
+        reps = max(1, int(round(seconds * cores / (per_cw * ncw))))
+
+        def work(i):
+            sl = slice((i * ncw) // cores, ((i + 1) * ncw) // cores)
+            for _ in range(reps):
+                orc.decode_deletion(rx[sl], ln[sl], self.n, self.n0, self.pd, fm, fv, self.ones)
+            return (sl.stop - sl.start) * reps
+
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(cores) as ex:
+            done = sum(ex.map(work, range(cores)))
+        dt = time.perf_counter() - t0
         return {"value": done / dt, "unit": "codewords/s", "cores": cores, "kind": "port",
-                "sample": "%d of the bench's own received words (time-bounded, %.0f s), oracle/trellis_oracle.py "
-                          "(pure Python) in one process per thread on %s" % (done, seconds, cdesc)}
-
-
-def _del_oracle_part(args):
-    words, n, n0, pd, fm, fv, seconds = args
-    sys.path.insert(0, ROOT)
-    from oracle import trellis_oracle as tro
-    t0 = time.perf_counter()
-    done = 0
-    for w in words:
-        tro.decode_deletion(w, n, n0, pd, fm, fv)
-        done += 1
-        if seconds and time.perf_counter() - t0 > seconds:
-            break
-    return done
+                "sample": "%d of the bench's own received words x %d passes, oracle/trellis_oracle.c (C restatement) "
+                          "on %s (%.1f CPU-s)" % (ncw, reps, cdesc, dt * cores)}
 
 
 class Qary:
@@ -351,13 +348,26 @@ class Qary:
             sc.set_qary_lds(bool(a.qlds))
 
         self.dec = sc.QaryDecoder(self.code)
-        info, self.xy = mc.philox_qsc_batch(self.code, a.seed, mc.rank_offset(rank, self.B), self.B, a.qsc_p)
+        self.tile = 0 if (a.no_tile or type(self) is not Qary) else self.dec.tile()
+        info, self.xy = mc.philox_qsc_batch(self.code, a.seed, mc.rank_offset(rank, self.B), self.B, a.qsc_p,
+                                            tile=self.tile)
         self.info_tx = info.t()
         self.dec.workspace(self.B)
         self.outs = None
 
     def step(self):
-        self.outs = self.dec.decode_native(self.xy)
+        if self.tile:
+            self.outs = self.dec.decode_tiled_native(self.xy, self.B)
+        else:
+            self.outs = self.dec.decode_native(self.xy)
+
+    def rows(self, ncw):
+        """The first ncw codewords' rows, [ncw, N, q] (the reference's layout)."""
+        if not self.tile:
+            return self.xy[:, :ncw, :].permute(1, 0, 2).contiguous()
+        T = self.tile
+        nt = (ncw + T - 1) // T
+        return self.xy[:nt].permute(0, 2, 1, 3).reshape(nt * T, self.N, self.q)[:ncw].contiguous()
 
     def errors(self):
         return mc.error_counts(self.outs[0].t(), self.info_tx)
@@ -375,10 +385,11 @@ class Qary:
                                                                                      self.B),
             dtype="f64",
             data="synthetic: uniform info symbols, GPU q-ary encoder, QSC(%.2f) on device (Philox keyed by global "
-                 "codeword index)" % self.a.qsc_p,
+                 "codeword index)%s" % (self.a.qsc_p, ", rows in %d-codeword tiles" % self.tile if self.tile else ""),
             config={"workload": "q-ary SC decode q=%d N=%d K=%d QSC(%.2f) (BASELINE configs[3])"
                                 % (self.q, self.N, self.K, self.a.qsc_p),
                     "N": self.N, "K": self.K, "q": self.q, "batch_per_gpu": self.B, "frozen_set": self.construction,
+                    "root_tile": self.tile,
                     "parallelism": "dp%d (codeword sharding, RCCL all_reduce of counters)" % world})
 
     def cpu_baseline(self, seconds=10.0):
@@ -389,7 +400,7 @@ class Qary:
         orc.lib()
         cores, cdesc = host_cores()
         ncw = 4096
-        sample = self.xy[:, :ncw, :].permute(1, 0, 2).contiguous().cpu().numpy()
+        sample = self.rows(ncw).cpu().numpy()
         t0 = time.perf_counter()
         orc.decode_qary(self.q, sample[:64], self.code.frozen_mask)
         per_cw = (time.perf_counter() - t0) / 64

@@ -87,6 +87,12 @@ int pcub_sc_decode_bin_tiled(const double* xy, int64_t B, int32_t log2N, int32_t
 size_t pcub_sc_decode_qary_workspace(int64_t B, int32_t log2N, int32_t q);
 int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, int32_t q, const uint8_t* frozen, int32_t K,
                         uint8_t* info, uint8_t* xhat, void* workspace, size_t workspace_bytes, void* stream);
+/* ... with the rows in tiles of T codewords ([ceil(B/T)][N][T][q], as pcub_sc_decode_bin_tiled);
+ * pcub_sc_qary_tile: the codewords one wave of the kernel decodes (the native T). */
+int pcub_sc_qary_tile(int32_t q, int32_t log2N);
+int pcub_sc_decode_qary_tiled(const double* xy, int64_t B, int32_t log2N, int32_t q, int32_t tile,
+                              const uint8_t* frozen, int32_t K, uint8_t* info, uint8_t* xhat, void* workspace,
+                              size_t workspace_bytes, void* stream);
 
 /* q-ary polar encoder (QaryPolarEncoderDecoder.py:65-88, frozen symbols 0):
  *   info [K][B] u8 -> x [N][B] u8, combine x[2h] = (xm+xp)%q, x[2h+1] = (q-xp)%q. */
@@ -290,6 +296,8 @@ size_t pcub_mc_run_bin_workspace(int64_t chunk, int32_t log2N, int32_t K);
 int pcub_mc_info_qary(uint64_t seed, int64_t offset, int64_t B, int32_t K, int32_t q, uint8_t* info, void* stream);
 int pcub_mc_channel_qsc(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t q, double p,
                         const uint8_t* x, double* xy, void* stream);
+int pcub_mc_channel_qsc_tiled(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t q, double p,
+                              const uint8_t* x, double* xy, int32_t tile, void* stream);
 int pcub_mc_deletion(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, const int32_t* tmpl, int32_t W,
                      double pd, const uint32_t* x_words, uint8_t* rx, int32_t* rx_len, void* stream);
 

@@ -1,4 +1,4 @@
-"""ctypes front-end for the CPU parity oracle (oracle/sc_oracle.c).
+"""ctypes front-end for the CPU parity oracle (oracle/sc_oracle.c, oracle/trellis_oracle.c).
 
 TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
 cpu_baseline leg of bench.py.  The product package (polarcub_amd) never imports
@@ -45,6 +45,10 @@ def lib():
                                                ctypes.c_int, _u8p, _u8p]
         L.orc_encode_qary.restype = None
         L.orc_encode_qary.argtypes = [ctypes.c_int, ctypes.c_int, _u8p, _u8p, _u8p]
+        L.orc_decode_deletion_batch.restype = ctypes.c_int
+        L.orc_decode_deletion_batch.argtypes = [_u8p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int64, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_double, _u8p, _u8p, ctypes.c_int,
+                                                ctypes.c_int, _u8p, _u8p]
         _lib = L
     return _lib
 
@@ -135,3 +139,23 @@ def encode_qary(q, info, frozen):
     x = np.zeros(frozen.shape[0], np.uint8)
     lib().orc_encode_qary(q, _log2(frozen.shape[0]), _p(frozen, _u8p), _p(info, _u8p), _p(x, _u8p))
     return x
+
+
+def decode_deletion(rx, rx_len, n, n0, pd, frozen, fval, ones=0):
+    """Deletion-channel SC decode of received words (oracle/trellis_oracle.c, the C restatement of
+    oracle/trellis_oracle.py).  rx: [B, W] u8 padded words, rx_len: [B].  Returns (info [B, K],
+    xhat [B, N])."""
+    rx = np.ascontiguousarray(rx, np.uint8)
+    ln = np.ascontiguousarray(rx_len, np.int32)
+    B, W = rx.shape
+    frozen = np.ascontiguousarray(frozen, np.uint8)
+    fval = np.ascontiguousarray(fval, np.uint8)
+    N = 1 << n
+    K = int(N - frozen.sum())
+    info = np.zeros((B, max(K, 1)), np.uint8)
+    xhat = np.zeros((B, N), np.uint8)
+    rc = lib().orc_decode_deletion_batch(_p(rx, _u8p), ln.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), B, W, n,
+                                         n0, float(pd), _p(frozen, _u8p), _p(fval, _u8p), int(ones), K,
+                                         _p(xhat, _u8p), _p(info, _u8p))
+    assert rc == 0, "orc_decode_deletion_batch failed"
+    return info[:, :K], xhat

@@ -153,6 +153,14 @@ def lib():
                                        _c_void_p]
     L.pcub_mc_info_qary.restype = ctypes.c_int
     L.pcub_mc_info_qary.argtypes = [_u64, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p]
+    L.pcub_mc_channel_qsc_tiled.restype = ctypes.c_int
+    L.pcub_mc_channel_qsc_tiled.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p, _i32,
+                                            _c_void_p]
+    L.pcub_sc_qary_tile.restype = ctypes.c_int
+    L.pcub_sc_qary_tile.argtypes = [_i32, _i32]
+    L.pcub_sc_decode_qary_tiled.restype = ctypes.c_int
+    L.pcub_sc_decode_qary_tiled.argtypes = [_c_void_p, _i64, _i32, _i32, _i32, _c_void_p, _i32, _c_void_p, _c_void_p,
+                                            _c_void_p, ctypes.c_size_t, _c_void_p]
     L.pcub_mc_channel_qsc.restype = ctypes.c_int
     L.pcub_mc_channel_qsc.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p, _c_void_p]
     L.pcub_mc_deletion.restype = ctypes.c_int
@@ -181,7 +189,8 @@ EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_b
            "pcub_mc_run_bin_workspace", "pcub_mc_run_bin", "pcub_sc_deletion_table_bytes",
            "pcub_sc_deletion_build_table", "pcub_sc_decode_deletion_tab", "pcub_sc_leaf_deletion_tab",
            "pcub_sc_set_deletion_dense", "pcub_sc_deletion_dense_layout", "pcub_sc_bin_tile", "pcub_sc_decode_bin_tiled",
-           "pcub_sc_decode_bin_compact_tiled", "pcub_mc_channel_tiled", "pcub_mc_channel_norm_tiled"]
+           "pcub_sc_decode_bin_compact_tiled", "pcub_mc_channel_tiled", "pcub_mc_channel_norm_tiled",
+           "pcub_mc_channel_qsc_tiled", "pcub_sc_qary_tile", "pcub_sc_decode_qary_tiled"]
 
 
 def check(rc, what):

@@ -120,6 +120,19 @@ __device__ __forceinline__ double2 bsc_pair(const McArgs& A, uint32_t xb, double
     return o;
 }
 
+// Two standard normals from two uniforms in (0, 1] (Box-Muller).  The transcendentals run in f32:
+// the noise is a simulation draw, not a reference value, and the f32 forms (v_log_f32, v_sqrt_f32,
+// sin / cos by pi-scaled reduction) are a few VALU each where the f64 log, sqrt and sincospi took
+// ~150 of the channel kernel's ~190 f64 instructions a pair.  u0 keeps its 53-bit resolution down
+// to the tail (u0 >= 2^-53 -> |z| <= 8.6), the 24-bit mantissa only rounds z (relative 6e-8).
+__device__ __forceinline__ void box_muller(double u0, double u1, double& z0, double& z1) {
+    const float rad = sqrtf(-2.0f * logf((float)u0));
+    float sn, cs;
+    sincospif(2.0f * (float)u1, &sn, &cs);
+    z0 = (double)(rad * cs);
+    z1 = (double)(rad * sn);
+}
+
 // grid: x over codewords, y strides over element pairs (a 2-D grid keeps every
 // dimension far below the 32-bit dispatch limits at N = 2^24).
 __global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_t* x, double2* xy) {
@@ -136,11 +149,10 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_
         const double u0 = u01(r.v[0], r.v[1]), u1 = u01(r.v[2], r.v[3]);
         double2 o0, o1;
         if (A.channel == 0) {
-            const double rad = sqrt(-2.0 * log(u0));
-            double sn, cs;
-            sincospi(2.0 * u1, &sn, &cs);  // sin, cos of 2 pi u1 (pi-scaled reduction)
-            o0 = awgn_pair(A, xw & 1u, rad * cs);
-            o1 = awgn_pair(A, (xw >> 1) & 1u, rad * sn);
+            double z0, z1;
+            box_muller(u0, u1, z0, z1);
+            o0 = awgn_pair(A, xw & 1u, z0);
+            o1 = awgn_pair(A, (xw >> 1) & 1u, z1);
         } else {
             o0 = bsc_pair(A, xw & 1u, u0);
             o1 = bsc_pair(A, (xw >> 1) & 1u, u1);
@@ -191,11 +203,10 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel_norm(McArgs A, const ui
         const double u0 = u01(r.v[0], r.v[1]), u1 = u01(r.v[2], r.v[3]);
         double c0, c1;
         if (A.channel == 0) {
-            const double rad = sqrt(-2.0 * log(u0));
-            double sn, cs;
-            sincospi(2.0 * u1, &sn, &cs);  // sin, cos of 2 pi u1 (pi-scaled reduction)
-            c0 = awgn_norm(A, xw & 1u, rad * cs);
-            c1 = awgn_norm(A, (xw >> 1) & 1u, rad * sn);
+            double z0, z1;
+            box_muller(u0, u1, z0, z1);
+            c0 = awgn_norm(A, xw & 1u, z0);
+            c1 = awgn_norm(A, (xw >> 1) & 1u, z1);
         } else {
             c0 = bsc_norm(A, xw & 1u, u0);
             c1 = bsc_norm(A, (xw >> 1) & 1u, u1);
@@ -270,7 +281,7 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_qsc(McArgs A, int q, const uint
         const int xs = x[i * A.B + b];
         const bool err = u01(r.v[0], r.v[1]) <= A.param;
         const int y = err ? (xs + 1 + (int)below(r.v[2], q - 1)) % q : xs;
-        double* row = xy + (i * A.B + b) * q;
+        double* row = xy + row_at(A, i, b) * q;
         for (int t = 0; t < q; ++t) row[t] = t == y ? hit : miss;
     }
 }
@@ -385,13 +396,14 @@ extern "C" int pcub_mc_info_qary(uint64_t seed, int64_t offset, int64_t B, int32
     return (int)hipGetLastError();
 }
 
-extern "C" int pcub_mc_channel_qsc(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t q, double p,
-                                   const uint8_t* x, double* xy, void* stream) {
+extern "C" int pcub_mc_channel_qsc_tiled(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t q, double p,
+                                         const uint8_t* x, double* xy, int32_t tile, void* stream) {
     if (B < 0 || offset < 0 || log2N < 0 || log2N > 24 || q < 2 || q > 255 || !(p >= 0.0 && p <= 1.0))
         return PCUB_EINVAL;
+    if (tile < 0 || tile > 4096) return PCUB_EINVAL;
     if (B == 0) return 0;
     if (!x || !xy) return PCUB_EINVAL;
-    McArgs A{seed, offset, B, log2N, 0, 2, p, 0.0, 0.0, 0.0, 0};
+    McArgs A{seed, offset, B, log2N, 0, 2, p, 0.0, 0.0, 0.0, tile};
     const long long gx = (B + kMcBlock - 1) / kMcBlock;
     long long gy = (16384 + gx - 1) / gx;
     if (gy > ((long long)1 << log2N)) gy = (long long)1 << log2N;
@@ -400,6 +412,11 @@ extern "C" int pcub_mc_channel_qsc(uint64_t seed, int64_t offset, int64_t B, int
     hipLaunchKernelGGL(k_mc_qsc, dim3((unsigned)gx, (unsigned)gy), dim3(kMcBlock), 0, (hipStream_t)stream, A, (int)q,
                        x, xy);
     return (int)hipGetLastError();
+}
+
+extern "C" int pcub_mc_channel_qsc(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, int32_t q, double p,
+                                   const uint8_t* x, double* xy, void* stream) {
+    return pcub_mc_channel_qsc_tiled(seed, offset, B, log2N, q, p, x, xy, 0, stream);
 }
 
 extern "C" int pcub_mc_deletion(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, const int32_t* tmpl,

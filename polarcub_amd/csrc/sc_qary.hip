@@ -168,10 +168,11 @@ extern "C" size_t pcub_sc_decode_qary_workspace(int64_t B, int32_t log2N, int32_
     return qtable_bytes(log2N, q) + (size_t)qgrid(B, q, log2N) * kQBlock * qslot_bytes(log2N, q);
 }
 
-extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, int32_t q, const uint8_t* frozen,
-                                   int32_t K, uint8_t* info, uint8_t* xhat, void* workspace, size_t workspace_bytes,
-                                   void* stream) {
-    if (B < 0 || log2N < 2 || log2N > 20 || !qkernel(q, log2N) || !frozen) return PCUB_EINVAL;
+namespace {
+
+int decode_qary_impl(const double* xy, int64_t B, int32_t log2N, int32_t q, int32_t tile, const uint8_t* frozen,
+                     int32_t K, uint8_t* info, uint8_t* xhat, void* workspace, size_t workspace_bytes, void* stream) {
+    if (B < 0 || log2N < 2 || log2N > 20 || !qkernel(q, log2N) || !frozen || tile < 0 || tile > 4096) return PCUB_EINVAL;
     if (K < 0 || K > (1 << log2N) || (K > 0 && !info) || (B > 0 && !xy)) return PCUB_EINVAL;
     if (B == 0) return 0;
     long long g = qgrid(B, q, log2N);
@@ -200,11 +201,32 @@ extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, i
     A.xhat = xhat;
     A.nslots = g * kQBlock;
     A.ylds_words = c.yl ? (int)(qsym_lds_bytes(log2N, c.G) / kQBlock / sizeof(uint32_t)) : 0;
+    A.tile = tile;
     char* slots = (char*)workspace + tb;
     A.scratch = (double2*)slots;
     A.ysym = c.yl ? nullptr : (uint32_t*)(slots + (size_t)A.nslots * (N / c.G - 2 * c.sr()) * ((q + 1) / 2) * sizeof(double2));
     hipLaunchKernelGGL(qkernel(q, log2N), dim3((unsigned)g), dim3(kQBlock), qlaunch_lds(q, log2N), st, A);
     return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int pcub_sc_decode_qary(const double* xy, int64_t B, int32_t log2N, int32_t q, const uint8_t* frozen,
+                                   int32_t K, uint8_t* info, uint8_t* xhat, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
+    return decode_qary_impl(xy, B, log2N, q, 0, frozen, K, info, xhat, workspace, workspace_bytes, stream);
+}
+
+// the codewords one wave of the q-ary kernel at (q, 2^log2N) decodes: the native tile width
+extern "C" int pcub_sc_qary_tile(int32_t q, int32_t log2N) {
+    if (log2N < 2 || log2N > 20 || !qkernel(q, log2N)) return PCUB_EINVAL;
+    return 64 / q_geom(q, log2N).G;
+}
+
+extern "C" int pcub_sc_decode_qary_tiled(const double* xy, int64_t B, int32_t log2N, int32_t q, int32_t tile,
+                                         const uint8_t* frozen, int32_t K, uint8_t* info, uint8_t* xhat,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+    return decode_qary_impl(xy, B, log2N, q, tile, frozen, K, info, xhat, workspace, workspace_bytes, stream);
 }
 
 extern "C" int pcub_polar_encode_qary(const uint8_t* info, int64_t B, int32_t log2N, int32_t q, const uint8_t* frozen,

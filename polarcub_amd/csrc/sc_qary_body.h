@@ -148,6 +148,7 @@ struct QArgs {
     uint32_t* ysym;          // [N/G/4 words][nslots], symbol of position p in byte p % 4 of word p / 4
     long long nslots;
     int ylds_words;          // symbol words per thread in LDS (YL kernels; the HL column follows them)
+    int tile;                // root layout: 0 = [N][B][Q]; T > 0 = [ceil(B/T)][N][T][Q] (T codewords a tile)
 };
 
 // Re-encoded symbols, four per word.  SWAR on bytes: every byte holds a value
@@ -485,7 +486,10 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
     uint32_t* Y = YL ? ylds : A.ysym + slot;
     const long long ys = YL ? ystride : ns;  // symbol word stride
     // root rows of lane j: real position j + G*t is row bitrev_n(j) + bitrev_{nv}(t)
-    const double* in = A.xy + (cw + (long long)bitrev((uint32_t)j, A.n) * A.B) * Q;
+    // tiled layout: codeword cw's row 0 at ((cw / T) N) T + cw % T, rows T apart
+    const long long rs = A.tile > 0 ? (long long)A.tile : A.B;
+    const long long rb = A.tile > 0 ? (cw / A.tile) * ((long long)A.tile << A.n) + cw % A.tile : cw;
+    const double* in = A.xy + (rb + (long long)bitrev((uint32_t)j, A.n) * rs) * Q;
     QInfo qi{A.info, A.B, cw, store, 0, j, G - 1, 0u};
     for (int k = 0; k < (1 << D); ++k) {
         in = launder(in);
@@ -498,7 +502,7 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
         bool gop = (k != 0);
         QPass P;
         P.in = in;
-        P.B = A.B;
+        P.B = rs;
         P.nv = nv;
         P.ns = ns;
         P.Y = Y;

@@ -181,10 +181,11 @@ def run_bin(code, seed, offset, count, channel, param, chunk=1 << 18):
     return [int(v) for v in counters.tolist()]
 
 
-def philox_qsc_batch(code, seed, offset, B, p):
+def philox_qsc_batch(code, seed, offset, B, p, tile=0):
     """q-ary information [K, B] u8 and QSC(p) joint rows [N, B, q] for global codewords
     [offset, offset + B) (pcub_mc_info_qary -> pcub_polar_encode_qary -> pcub_mc_channel_qsc);
-    the same codewords whichever rank or chunk generates them."""
+    the same codewords whichever rank or chunk generates them.  tile = T > 0: the rows in the tiled
+    layout [ceil(B/T), N, T, q] (QaryDecoder.decode_tiled_native)."""
     from . import _lib
     L = _lib.lib()
     dev = code.device
@@ -194,9 +195,12 @@ def philox_qsc_batch(code, seed, offset, B, p):
     x = torch.empty((code.N, B), dtype=torch.uint8, device=dev)
     _lib.check(L.pcub_polar_encode_qary(sc._p(info), B, code.n, code.q, sc._p(code.frozen_dev), code.K, sc._p(x),
                                         sc._stream()), "pcub_polar_encode_qary")
-    xy = torch.empty((code.N, B, code.q), dtype=torch.float64, device=dev)
-    _lib.check(L.pcub_mc_channel_qsc(int(seed), int(offset), B, code.n, code.q, float(p), sc._p(x), sc._p(xy),
-                                     sc._stream()), "pcub_mc_channel_qsc")
+    if tile:
+        xy = torch.zeros(((B + tile - 1) // tile, code.N, tile, code.q), dtype=torch.float64, device=dev)
+    else:
+        xy = torch.empty((code.N, B, code.q), dtype=torch.float64, device=dev)
+    _lib.check(L.pcub_mc_channel_qsc_tiled(int(seed), int(offset), B, code.n, code.q, float(p), sc._p(x), sc._p(xy),
+                                           int(tile), sc._stream()), "pcub_mc_channel_qsc_tiled")
     return info[:code.K], xy
 
 

@@ -503,6 +503,28 @@ class QaryDecoder:
         _lib.check(rc, "pcub_sc_decode_qary")
         return info[:c.K], xh
 
+    def tile(self):
+        """The native tile width of the tiled root layout (pcub_sc_qary_tile)."""
+        return int(_lib.lib().pcub_sc_qary_tile(self.code.q, self.code.n))
+
+    def decode_tiled_native(self, xy_t, B, want_xhat=True):
+        """xy_t: [ceil(B/T), N, T, q] float64 on device (tile_rows of the [N, B, q] rows), B codewords:
+        the same decode as decode_native, each wave's codewords read as one contiguous block."""
+        c = self.code
+        if xy_t.dtype != torch.float64 or xy_t.dim() != 4 or xy_t.shape[1] != c.N or xy_t.shape[3] != c.q:
+            raise ValueError("xy_t must be float64 [ceil(B/T), N, T, q] with N=%d, q=%d" % (c.N, c.q))
+        T = xy_t.shape[2]
+        if xy_t.shape[0] != (B + T - 1) // T:
+            raise ValueError("xy_t holds %d tiles of %d codewords; B=%d" % (xy_t.shape[0], T, B))
+        xy_t = xy_t.contiguous()
+        info = torch.empty((max(1, c.K), B), dtype=torch.uint8, device=xy_t.device)
+        xh = torch.empty((c.N, B), dtype=torch.uint8, device=xy_t.device) if want_xhat else None
+        ws = self.workspace(B)
+        rc = _lib.lib().pcub_sc_decode_qary_tiled(_p(xy_t), B, c.n, c.q, T, _p(c.frozen_dev), c.K, _p(info), _p(xh),
+                                                  _p(ws), ws.numel(), _stream())
+        _lib.check(rc, "pcub_sc_decode_qary_tiled")
+        return info[:c.K], xh
+
     def decode(self, xy):
         """xy: [B, N, q] float64 -> (info [B, K] uint8, xhat [B, N] uint8)."""
         info, xh = self.decode_native(transpose_pairs(xy))

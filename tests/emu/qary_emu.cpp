@@ -49,6 +49,7 @@ static int run(const double* xy, long long B, int n, const uint8_t* frozen, uint
     A.ysym = ys.data();
     A.nslots = ns;
     A.ylds_words = 0;
+    A.tile = 0;
     if (hl) {
         switch (S) {
             case 1: run_h<Q, 1>(A, B); break;

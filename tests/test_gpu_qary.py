@@ -88,3 +88,22 @@ def test_qary_facade_decode():
         info = encdec.decode(xvd, yvd)
         assert info.dtype == np.int64 and np.array_equal(info, g["info"][t])
     assert np.array_equal(encdec.encode(xvd, list(g["tx_info"][0])), g["x"][0])
+
+
+@pytest.mark.parametrize("q", [2, 3, 4, 8])
+def test_tiled_root_layout_qary(q):
+    """pcub_sc_decode_qary_tiled: the rows in tiles of T codewords (the native width, 1, 5) decode
+    exactly as the [N, B, q] rows, ragged last tiles included."""
+    import torch
+    from polarcub_amd import sc
+    rng = np.random.default_rng(40 + q)
+    for N, B in [(16, 50), (256, 333)]:
+        frozen = (rng.random(N) < 0.5).astype(np.uint8)
+        code = sc.QaryCode(q, N, frozen, device="cuda")
+        dec = sc.QaryDecoder(code)
+        xy = rng.random((N, B, q))
+        native = torch.from_numpy(xy).cuda()
+        ri, rx = dec.decode_native(native)
+        for T in sorted({dec.tile(), 1, 5}):
+            ti, tx = dec.decode_tiled_native(sc.tile_rows(native, T), B)
+            assert torch.equal(ti, ri) and torch.equal(tx, rx), (N, T)

@@ -101,3 +101,45 @@ def _polar(u):
     for i in range(h):
         out += [(xm[i] + xp[i]) % 2, xp[i]]
     return out
+
+
+# -- the C restatement (oracle/trellis_oracle.c): pinned to the same reference outputs and to the
+#    Python restatement on random shapes; bench.py times it as the deletion CPU baseline.
+
+def _padded(words):
+    W = max([len(w) for w in words] + [1])
+    rx = np.zeros((len(words), W), np.uint8)
+    for i, w in enumerate(words):
+        rx[i, :len(w)] = w
+    return rx, np.array([len(w) for w in words], np.int32)
+
+
+def test_c_oracle_matches_reference():
+    from oracle import orc
+    g = load_golden("deletion_n8")
+    m = g["meta"]
+    info, xhat = orc.decode_deletion(g["rx"], g["rx_len"], m["n"], m["n0"], m["pd"], g["frozen"], g["fval"], m["ones"])
+    assert np.array_equal(info, g["info"]) and np.array_equal(xhat, g["xhat"])
+    for c in deletion_edge_cases():
+        n, n0, ones = (int(v) for v in c["shape"])
+        info, xhat = orc.decode_deletion(c["rx"], c["rx_len"], n, n0, float(c["pd"][0]), c["frozen"], c["fval"], ones)
+        assert np.array_equal(info, c["info"]) and np.array_equal(xhat, c["xhat"])
+
+
+@pytest.mark.parametrize("n,n0,ones", [(6, 2, 0), (8, 2, 0), (9, 3, 0), (10, 3, 0), (8, 2, 2), (7, 1, 0), (8, 4, 0),
+                                       (5, 5, 1)])
+def test_c_oracle_matches_python_oracle(n, n0, ones):
+    from oracle import orc
+    rng = np.random.default_rng(10 * n + n0 + ones)
+    prng = random.Random(n + n0)
+    N = 1 << n
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    words = [tro.deletion_channel(tro.add_guard_bands([int(b) for b in rng.integers(0, 2, N)], n, n0, 0.1, ones), 0.1,
+                                  prng) for _ in range(5)]
+    words += [[], [1], [0, 0, 1], [1] * (N + 3)]
+    rx, ln = _padded(words)
+    info, xhat = orc.decode_deletion(rx, ln, n, n0, 0.1, frozen, fval, ones)
+    for i, w in enumerate(words):
+        x, inf = tro.decode_deletion(w, n, n0, 0.1, frozen, fval, ones)
+        assert list(info[i]) == inf and list(xhat[i]) == x, i

@@ -41,8 +41,7 @@ KernFn variant_kernel(int v) {
     if (KernFn k = bin_kernel_part2(v)) return k;
     if (KernFn k = bin_kernel_part3(v)) return k;
     if (KernFn k = bin_kernel_part4(v)) return k;
-    if (KernFn k = bin_kernel_part5(v)) return k;
-    return bin_kernel_part6(v);
+    return bin_kernel_part5(v);
 }
 
 // {32, 4, 2, NT, re-encoded bits in LDS, split last level, prefetch 2}: at N=1024 one stored

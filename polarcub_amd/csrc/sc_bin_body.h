@@ -122,10 +122,7 @@ PCUB_HD double xor_shfl_c(double v) { return v; }  // host emulation runs G = 1 
 // A real node of length M (M <= G) with position (lane & (M-1)) held by each lane.
 // Returns this lane's bit of the node's (half-split) encoding; ORs the M
 // decisions u_UBASE .. u_UBASE+M-1 (identical in all lanes) into ub.
-// SPX: the plus child's input is evaluated for both values of the minus child's bit beside the
-// minus transform (op_g2) and picked once the bit is known, so the serial chain of a leaf holds
-// one division per level instead of two (the values are op_g's, bit for bit).
-template <int M, int UBASE, bool SPX = false>
+template <int M, int UBASE>
 struct XSub {
     static PCUB_HD uint32_t run(double v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane) {
         const double w = xor_shfl_c<M / 2>(v);
@@ -140,29 +137,6 @@ struct XSub {
             const uint32_t u1 = ((fm >> (UBASE + 1)) & 1u) ? (uint32_t)((fv >> (UBASE + 1)) & 1u) : (u0 ? d11 : d10);
             ub |= ((uint64_t)u0 << UBASE) | ((uint64_t)u1 << (UBASE + 1));
             return lo ? (u0 ^ u1) : u1;
-        } else if constexpr (SPX) {
-            constexpr int H = M / 2;
-            constexpr uint64_t HM = (1ull << H) - 1ull;
-            const int pos = lane & (H - 1);
-            const bool fl = all_frozen<H>(fm, UBASE), fr = all_frozen<H>(fm, UBASE + H);
-            uint32_t ym, yp;
-            double g0 = 0.0, g1 = 0.0;
-            if (fl) {
-                ym = frozen_local<1, H>(fv >> UBASE, pos) & 1u;
-                ub |= fv & (HM << UBASE);
-                if (!fr) g0 = g1 = op_g(a, b, ym);
-            } else {
-                const double c = op_f(a, b);
-                if (!fr) op_g2(a, b, g0, g1);
-                ym = XSub<H, UBASE, true>::run(c, ub, fm, fv, lane);
-            }
-            if (fr) {
-                yp = frozen_local<1, H>(fv >> (UBASE + H), pos) & 1u;
-                ub |= fv & (HM << (UBASE + H));
-            } else {
-                yp = XSub<H, UBASE + H, true>::run(g_pick(g0, g1, ym), ub, fm, fv, lane);
-            }
-            return lo ? (ym ^ yp) : yp;
         } else {
             // a frozen child (wave-uniform test) is not evaluated: its decisions are
             // the frozen values and its encoding their polar transform
@@ -189,16 +163,12 @@ struct XSub {
 
 // Register-resident virtual subtree of L values per lane; virtual leaf BASE_V
 // covers real u positions [BASE_V*G, BASE_V*G + G).  Returns L local encoding bits.
-// SP: nodes of at most SP values per lane evaluate their plus child's input for both decisions
-// beside the minus transform (op_g2) and pick it once the minus subtree has decided; the
-// cross-lane leaves (XSub) and leaf pairs do the same when SP > 0.  The pair g0/g1 replaces the
-// node's own values across the minus subtree, so the registers live there are as many as before.
-template <int L, int BASE_V, int G, int SP = 0>
+template <int L, int BASE_V, int G>
 struct SubV {
     static PCUB_HD uint32_t run(const double* v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane) {
         if constexpr (L == 1) {
             static_assert(G >= 2, "G == 1 stops at L == 2");
-            return XSub<G, BASE_V * G, (SP > 0)>::run(v[0], ub, fm, fv, lane);
+            return XSub<G, BASE_V * G>::run(v[0], ub, fm, fv, lane);
         } else if constexpr (L == 2 && G == 1) {
             uint32_t d0, d10, d11;
             leaf_pair(v[0], v[1], d0, d10, d11);
@@ -217,50 +187,21 @@ struct SubV {
             const int j = lane & (G - 1);
             double c[H];
             uint32_t ym, yp;
-            const bool fl = all_frozen<HR>(fm, BASE_V * G), fr = all_frozen<HR>(fm, (BASE_V + H) * G);
-            if constexpr (L <= SP) {
-                double g0[H], g1[H];
-                if (fl) {
-                    ym = frozen_local<H, G>(fv >> (BASE_V * G), j) & LMASK;
-                    ub |= fv & (HM << (BASE_V * G));
-                    if (!fr) {
-#pragma unroll
-                        for (int t = 0; t < H; ++t) g1[t] = g0[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
-                    }
-                } else {
-#pragma unroll
-                    for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
-                    if (!fr) {
-#pragma unroll
-                        for (int t = 0; t < H; ++t) op_g2(v[t], v[t + H], g0[t], g1[t]);
-                    }
-                    ym = SubV<H, BASE_V, G, SP>::run(c, ub, fm, fv, lane);
-                }
-                if (fr) {
-                    yp = frozen_local<H, G>(fv >> ((BASE_V + H) * G), j) & LMASK;
-                    ub |= fv & (HM << ((BASE_V + H) * G));
-                } else {
-#pragma unroll
-                    for (int t = 0; t < H; ++t) c[t] = g_pick(g0[t], g1[t], (ym >> t) & 1u);
-                    yp = SubV<H, BASE_V + H, G, SP>::run(c, ub, fm, fv, lane);
-                }
+            if (all_frozen<HR>(fm, BASE_V * G)) {
+                ym = frozen_local<H, G>(fv >> (BASE_V * G), j) & LMASK;
+                ub |= fv & (HM << (BASE_V * G));
             } else {
-                if (fl) {
-                    ym = frozen_local<H, G>(fv >> (BASE_V * G), j) & LMASK;
-                    ub |= fv & (HM << (BASE_V * G));
-                } else {
 #pragma unroll
-                    for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
-                    ym = SubV<H, BASE_V, G, SP>::run(c, ub, fm, fv, lane);
-                }
-                if (fr) {
-                    yp = frozen_local<H, G>(fv >> ((BASE_V + H) * G), j) & LMASK;
-                    ub |= fv & (HM << ((BASE_V + H) * G));
-                } else {
+                for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
+                ym = SubV<H, BASE_V, G>::run(c, ub, fm, fv, lane);
+            }
+            if (all_frozen<HR>(fm, (BASE_V + H) * G)) {
+                yp = frozen_local<H, G>(fv >> ((BASE_V + H) * G), j) & LMASK;
+                ub |= fv & (HM << ((BASE_V + H) * G));
+            } else {
 #pragma unroll
-                    for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
-                    yp = SubV<H, BASE_V + H, G, SP>::run(c, ub, fm, fv, lane);
-                }
+                for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
+                yp = SubV<H, BASE_V + H, G>::run(c, ub, fm, fv, lane);
             }
             return (ym ^ yp) | (yp << H);
         }
@@ -414,21 +355,6 @@ PCUB_HD T* launder(T* p) {
     return p;
 }
 
-// A wave-uniform integer made opaque at this point (kept in SGPRs): the root row offsets of a pass
-// derive from it, so they are formed inside the pass, next to their loads, instead of being
-// hoisted out of the whole schedule as 128 loop-invariant 64-bit values (466 spilled SGPRs,
-// reloaded by v_readlane before every root load).
-PCUB_HD long long launder_s(long long x) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(PCUB_LAUNDER_B)
-    int lo = __builtin_amdgcn_readfirstlane((int)(unsigned long long)x);
-    int hi = __builtin_amdgcn_readfirstlane((int)((unsigned long long)x >> 32));
-    asm volatile("" : "+s"(lo), "+s"(hi));
-    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-#else
-    return x;
-#endif
-}
-
 // Keeps the scheduler from hoisting the next column's loads above this point
 // (bounds the live registers of the unrolled final pass).
 PCUB_HD void sched_fence() {
@@ -440,56 +366,29 @@ PCUB_HD void sched_fence() {
 // A register subtree's u decisions and frozen bits live in NW 64-bit windows
 // (NW = S*G/64 when the subtree has more than 64 real positions): WinTree splits
 // the subtree at its top nodes until each part is one window.
-template <int L, int G, int NWIN, int SP = 0>
+template <int L, int G, int NWIN>
 struct WinTree {
     static PCUB_HD uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm, const uint64_t* fv, int lane) {
         if constexpr (NWIN == 1) {
-            return SubV<L, 0, G, SP>::run(v, ub[0], fm[0], fv[0], lane);
+            return SubV<L, 0, G>::run(v, ub[0], fm[0], fv[0], lane);
         } else {
             constexpr int H = L / 2;
             constexpr int HW = NWIN / 2;
             double c[H];
             uint32_t ym, yp;
-            const bool fl = frozen_windows(fm), fr = frozen_windows(fm + HW);
-            if constexpr (L <= SP) {
-                double g0[H], g1[H];
-                if (fl) {
-                    ym = WinTree<H, G, HW, SP>::frozen(ub, fv, lane & (G - 1));
-                    if (!fr) {
-#pragma unroll
-                        for (int t = 0; t < H; ++t) g1[t] = g0[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
-                    }
-                } else {
-#pragma unroll
-                    for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
-                    if (!fr) {
-#pragma unroll
-                        for (int t = 0; t < H; ++t) op_g2(v[t], v[t + H], g0[t], g1[t]);
-                    }
-                    ym = WinTree<H, G, HW, SP>::run(c, ub, fm, fv, lane);
-                }
-                if (fr) {
-                    yp = WinTree<H, G, HW, SP>::frozen(ub + HW, fv + HW, lane & (G - 1));
-                } else {
-#pragma unroll
-                    for (int t = 0; t < H; ++t) c[t] = g_pick(g0[t], g1[t], (ym >> t) & 1u);
-                    yp = WinTree<H, G, HW, SP>::run(c, ub + HW, fm + HW, fv + HW, lane);
-                }
+            if (frozen_windows(fm)) {
+                ym = WinTree<H, G, HW>::frozen(ub, fv, lane & (G - 1));
             } else {
-                if (fl) {
-                    ym = WinTree<H, G, HW, SP>::frozen(ub, fv, lane & (G - 1));
-                } else {
 #pragma unroll
-                    for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
-                    ym = WinTree<H, G, HW, SP>::run(c, ub, fm, fv, lane);
-                }
-                if (fr) {
-                    yp = WinTree<H, G, HW, SP>::frozen(ub + HW, fv + HW, lane & (G - 1));
-                } else {
+                for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
+                ym = WinTree<H, G, HW>::run(c, ub, fm, fv, lane);
+            }
+            if (frozen_windows(fm + HW)) {
+                yp = WinTree<H, G, HW>::frozen(ub + HW, fv + HW, lane & (G - 1));
+            } else {
 #pragma unroll
-                    for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
-                    yp = WinTree<H, G, HW, SP>::run(c, ub + HW, fm + HW, fv + HW, lane);
-                }
+                for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
+                yp = WinTree<H, G, HW>::run(c, ub + HW, fm + HW, fv + HW, lane);
             }
             return (ym ^ yp) | (yp << H);
         }
@@ -511,8 +410,8 @@ struct WinTree {
             return frozen_local<L, G>(fv[0], j);
         } else {
             constexpr int H = L / 2;
-            const uint32_t ym = WinTree<H, G, NWIN / 2, SP>::frozen(ub, fv, j);
-            const uint32_t yp = WinTree<H, G, NWIN / 2, SP>::frozen(ub + NWIN / 2, fv + NWIN / 2, j);
+            const uint32_t ym = WinTree<H, G, NWIN / 2>::frozen(ub, fv, j);
+            const uint32_t yp = WinTree<H, G, NWIN / 2>::frozen(ub + NWIN / 2, fv + NWIN / 2, j);
             return (ym ^ yp) | (yp << H);
         }
     }

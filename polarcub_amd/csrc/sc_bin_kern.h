@@ -19,12 +19,10 @@ constexpr int kBinBlock = 256;
 // in LDS (Nv/32 words per thread; only where W workgroups still fit a CU's LDS).
 // H = the chain's last level has 2S values per lane, the first S in LDS (HL; hl_run).
 // P = prefetch distance of the final passes, in column pairs (chain_final).
-// X = speculative plus transforms (op_g2) in register nodes of at most X values per lane and, for
-// X > 0, in the cross-lane leaves; Q = the same at the split level (hl_run).
 struct Variant {
-    int S, G, W, L, T, Y, H, P, X, Q;
+    int S, G, W, L, T, Y, H, P;
 };
-constexpr int kNumVariants = 38;
+constexpr int kNumVariants = 33;
 constexpr Variant kVar[kNumVariants] = {
     {16, 1, 2, 0, 0}, {8, 1, 4, 0, 0}, {32, 1, 1, 0, 0}, {16, 4, 2, 0, 0}, {8, 4, 4, 0, 0}, {16, 2, 2, 0, 0},
     {32, 2, 1, 0, 0}, {8, 8, 4, 0, 0}, {16, 2, 2, 0, 1}, {8, 8, 4, 0, 1}, {16, 4, 2, 0, 1}, {8, 4, 4, 1, 0},
@@ -34,8 +32,6 @@ constexpr Variant kVar[kNumVariants] = {
     {32, 4, 3, 0, 1, 1}, {32, 8, 3, 0, 1, 1},
     {32, 4, 2, 0, 1, 1, 1, 2}, {32, 4, 2, 0, 1, 1, 1, 1}, {32, 4, 2, 0, 1, 1, 1, 3}, {32, 4, 3, 0, 1, 1, 0, 2},
     {32, 8, 2, 0, 1, 1, 1, 2}, {32, 4, 2, 0, 1, 0, 1, 2}, {16, 8, 3, 0, 1, 1, 1, 2},
-    {32, 4, 2, 0, 1, 1, 1, 2, 1, 0}, {32, 4, 2, 0, 1, 1, 1, 2, 4, 0}, {32, 4, 2, 0, 1, 1, 1, 2, 16, 0},
-    {32, 4, 2, 0, 1, 1, 1, 2, 32, 0}, {32, 4, 2, 0, 1, 1, 1, 2, 32, 1},
 };
 
 // LDS bytes of the stage level (L: S pairs per thread) or of the split level's LDS half (H: S doubles)
@@ -52,8 +48,7 @@ inline size_t bin_ylds_bytes(int v, int n) {
     return kVar[v].Y ? (size_t)kBinBlock * (((size_t)1 << n) / kVar[v].G / 32) * sizeof(uint32_t) : 0;
 }
 
-template <int S, int G, int W, bool LDS, int NT, bool YL = false, bool HL = false, int PF = 0, bool CR = false,
-          int SP = 0, bool HSP = false>
+template <int S, int G, int W, bool LDS, int NT, bool YL = false, bool HL = false, int PF = 0, bool CR = false>
 __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
     // [S pairs][kBinBlock] when LDS (HL: [S doubles][kBinBlock]), then [Nv/32 words][kBinBlock]
     // when YL (plus occupancy padding)
@@ -68,7 +63,7 @@ __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_codeword<S, G, LDS, NT, YL, HL, PF, CR, SP, HSP>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last,
+        decode_codeword<S, G, LDS, NT, YL, HL, PF, CR>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last,
                                                YL ? (uint32_t*)(lds_last + LDS2) + threadIdx.x : nullptr, kBinBlock,
                                                HL ? (double*)lds_last + threadIdx.x : nullptr);
     }
@@ -83,7 +78,6 @@ BinKernFn bin_kernel_part2(int v);
 BinKernFn bin_kernel_part3(int v);
 BinKernFn bin_kernel_part4(int v);
 BinKernFn bin_kernel_part5(int v);
-BinKernFn bin_kernel_part6(int v);
 // the compact-root twin of variant v (CR: root rows as compact normalised doubles), or nullptr
 BinKernFn bin_kernel_compact(int v);
 

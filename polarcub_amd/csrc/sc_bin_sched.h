@@ -130,13 +130,10 @@ PCUB_HD void chain_pass(const Chain& c, int La, const LevelMap& lm, int a) {
 #pragma unroll
     for (int e = 1; e <= F; ++e) lv[e - 1] = lm.get(a + e);
     const int C = La >> F;
-    Chain cc = c;  // as chain_final: row offsets formed in the pass
-    cc.B = launder_s(c.B);
-    cc.nv = (int)launder_s(c.nv);
 #pragma unroll 1
     for (int p = 0; p < C; p += 2) {
         double2 y[(1 << F) - 1];
-        colpair<F, FG, R, G, NS, true, YL>(cc, p, C, y);
+        colpair<F, FG, R, G, NS, true, YL>(c, p, C, y);
         int off = 0;
 #pragma unroll
         for (int e = 1; e <= F; ++e) {
@@ -166,15 +163,12 @@ PCUB_HD void chain_final(const Chain& c, const Lvl* lv, double* v, double* hl) {
     constexpr bool NSF = NS && F == 2;
     constexpr bool GLF = F == 2 || !LL;
     ColLoad<F, FG, R> L[PD + 1];
-    Chain cc = c;  // root row stride and code length opaque here: row offsets formed in the pass
-    cc.B = launder_s(c.B);
-    cc.nv = (int)launder_s(c.nv);
 #pragma unroll
-    for (int i = 0; i < PD; ++i) col_load<F, FG, R, NSF, GLF, YL>(cc, 2 * i, S, L[i]);
+    for (int i = 0; i < PD; ++i) col_load<F, FG, R, NSF, GLF, YL>(c, 2 * i, S, L[i]);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
         const int p = 2 * i;
-        if (i + PD < NP) col_load<F, FG, R, NSF, GLF, YL>(cc, 2 * (i + PD), S, L[(i + PD) % (PD + 1)]);
+        if (i + PD < NP) col_load<F, FG, R, NSF, GLF, YL>(c, 2 * (i + PD), S, L[(i + PD) % (PD + 1)]);
         double2 y[(1 << F) - 1];
         col_compute<F, FG, R>(L[i % (PD + 1)], y);
         if constexpr (F == 2) {
@@ -228,7 +222,7 @@ PCUB_HD int final_levels(int T) {
     return (T % 3 == 2) ? 2 : 1;
 }
 
-template <int S, int G, int SP = 0>
+template <int S, int G>
 struct SubWin {
     static constexpr int SU = S * G;
     static constexpr int NW = SU > 64 ? SU / 64 : 1;
@@ -238,61 +232,43 @@ struct SubWin {
 
     // decisions of the subtree from its S level-D values
     static PCUB_HD uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm, const uint64_t* fv, int lane) {
-        return WinTree<S, G, NW, SP>::run(v, ub, fm, fv, lane);
+        return WinTree<S, G, NW>::run(v, ub, fm, fv, lane);
     }
 
-    static PCUB_HD uint32_t frozen(uint64_t* ub, const uint64_t* fv, int j) { return WinTree<S, G, NW, SP>::frozen(ub, fv, j); }
+    static PCUB_HD uint32_t frozen(uint64_t* ub, const uint64_t* fv, int j) { return WinTree<S, G, NW>::frozen(ub, fv, j); }
 };
 
 // HL subtree: a virtual node of 2S values per lane, values 0..S-1 in the LDS column hl and
 // S..2S-1 in vr; its two S-value children are register subtrees (SubWin<S, G>, NW windows
 // each).  Returns the node's 2S local encoding bits.  The top minus/plus transforms read the
 // LDS half twice; everything below runs in registers as in the plain variants.
-// HSP: the plus child's inputs for both decisions (op_g2) are formed beside the minus transform
-// and overwrite the node in place (u = 0 in the LDS column, u = 1 in vr); the plus transform is
-// then a pick.
-template <int S, int G, int SP = 0, bool HSP = false>
-PCUB_HD uint64_t hl_run(double* hl, double* vr, uint64_t* ub, const uint64_t* fm, const uint64_t* fv, int lane) {
-    using W = SubWin<S, G, SP>;
+template <int S, int G>
+PCUB_HD uint64_t hl_run(const double* hl, const double* vr, uint64_t* ub, const uint64_t* fm, const uint64_t* fv,
+                        int lane) {
+    using W = SubWin<S, G>;
     constexpr int NW = W::NW;
     static_assert(S * G >= 64, "HL halves are whole 64-bit windows");
     const int j = lane & (G - 1);
     double c[S];
     uint32_t ym, yp;
-    bool fzm = true, fzp = true;
+    bool fz = true;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        fzm = fzm && (fm[w] == ~0ull);
-        fzp = fzp && (fm[NW + w] == ~0ull);
-    }
-    if (fzm) {
+    for (int w = 0; w < NW; ++w) fz = fz && (fm[w] == ~0ull);
+    if (fz) {
         ym = W::frozen(ub, fv, j);
     } else {
 #pragma unroll
         for (int t = 0; t < S; ++t) c[t] = op_f(ldl(hl + (long long)t * kHlStride), vr[t]);
-        if constexpr (HSP) {
-            if (!fzp) {
-#pragma unroll
-                for (int t = 0; t < S; ++t) {
-                    double g0, g1;
-                    op_g2(ldl(hl + (long long)t * kHlStride), vr[t], g0, g1);
-                    stl(hl + (long long)t * kHlStride, g0);
-                    vr[t] = g1;
-                }
-            }
-        }
         ym = W::run(c, ub, fm, fv, lane);
     }
-    if (fzp) {
+    fz = true;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) fz = fz && (fm[NW + w] == ~0ull);
+    if (fz) {
         yp = W::frozen(ub + NW, fv + NW, j);
     } else {
-        if (HSP && !fzm) {
 #pragma unroll
-            for (int t = 0; t < S; ++t) c[t] = g_pick(ldl(hl + (long long)t * kHlStride), vr[t], (ym >> t) & 1u);
-        } else {
-#pragma unroll
-            for (int t = 0; t < S; ++t) c[t] = op_g(ldl(hl + (long long)t * kHlStride), vr[t], (ym >> t) & 1u);
-        }
+        for (int t = 0; t < S; ++t) c[t] = op_g(ldl(hl + (long long)t * kHlStride), vr[t], (ym >> t) & 1u);
         yp = W::run(c, ub + NW, fm + NW, fv + NW, lane);
     }
     constexpr uint64_t SM = (S == 32) ? 0xffffffffull : ((1ull << S) - 1ull);
@@ -318,7 +294,7 @@ PCUB_HD uint64_t hl_frozen(uint64_t* ub, const uint64_t* fv, int j) {
 //     hl, second half in registers; hl_run), one stored stage depth fewer than the plain S
 // PF: prefetch distance of the final passes (column pairs whose loads are in flight ahead)
 template <int S, int G, bool LDS = false, int NT = 0, bool YL = false, bool HL = false, int PF = 0, bool CR = false,
-          int SP = 0, bool HSP = false, int PF1 = -1>
+          int PF1 = -1>
 PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
                              Lvl last = Lvl{nullptr, 0}, uint32_t* ylds = nullptr, long long ystride = 0,
                              double* hl = nullptr) {
@@ -330,7 +306,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     constexpr int g = (G == 1) ? 0 : (G == 2) ? 1 : (G == 4) ? 2 : (G == 8) ? 3 : 4;
     constexpr uint64_t SMASK = (SR == 64) ? ~0ull : ((1ull << SR) - 1ull);
     constexpr int SU = SR * G;  // real u positions per chain-end subtree (<= 256)
-    using W = SubWin<SR, G, SP>;   // window geometry (HL: the S-value halves run SubWin<S, G>)
+    using W = SubWin<SR, G>;   // window geometry (HL: the S-value halves run SubWin<S, G>)
     constexpr int NW = W::NW;
     constexpr int RR = CR ? 3 : NT >= 1 ? 2 : 1;  // root loads (CR: the compact root A.xc)
     constexpr bool NS = NT >= 2;
@@ -449,7 +425,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         }
         if constexpr (HL) {
             if (e0 == D) y = hl_frozen<S, G>(ub, fv, j);
-            else y = hl_run<S, G, SP, HSP>(hl, v, ub, fm, fv, lane);
+            else y = hl_run<S, G>(hl, v, ub, fm, fv, lane);
         } else {
             if (e0 == D) {  // the register subtree itself is rate-0 (its level-D values go unused)
                 y = W::frozen(ub, fv, j) & SMASK;

@@ -105,26 +105,6 @@ PCUB_HD double op_g(double va, double vb, uint32_t u) {
     return cv_pack(q, s);
 }
 
-// Both outcomes of op_g before u is known: g0 = op_g(va, vb, 0), g1 = op_g(va, vb, 1), bit for
-// bit.  (a.s ^ u) == b.s is the same-orientation case for exactly one u, so the pair costs one
-// product and one division whatever the orientations -- the work op_g does when the lanes of a
-// wave disagree -- and both are off the critical path: they depend on (va, vb) only, so they run
-// beside the minus transform of the same node instead of after the minus subtree's decisions.
-PCUB_HD void op_g2(double va, double vb, double& g0, double& g1) {
-    const CV a = cv_load(va), b = cv_load(vb);
-    const double gs = cv_pack(a.r * b.r, b.s);
-    const bool agt = a.r > b.r;
-    const double mx = agt ? a.r : b.r;
-    const double mn = agt ? b.r : a.r;
-    const uint32_t so = b.s ? (agt ? 1u : 0u) : (b.r > a.r ? 1u : 0u);
-    const double go = cv_pack(mn / mx, so);
-    const bool same0 = a.s == b.s;  // u = 0 keeps the orientations as they are
-    g0 = same0 ? gs : go;
-    g1 = same0 ? go : gs;
-}
-
-PCUB_HD double g_pick(double g0, double g1, uint32_t u) { return u ? g1 : g0; }
-
 // Leaf pair (a, b) = rows (2h, 2h+1) of a length-2 node: u0's decision (leaf_f) and u1's
 // decision (leaf_g) for both values of u0, from one product.
 PCUB_HD void leaf_pair(double va, double vb, uint32_t& d0, uint32_t& d1u0, uint32_t& d1u1) {

@@ -16,42 +16,7 @@
 
 using namespace pcub;
 
-#if defined(DIAG_XSUB)
-namespace pcub {
-// Diagnostic replacements of the cross-lane leaf subtree, entered by decode_codeword<.., SP = 1>.
-template <int UBASE>
-struct XSub<4, UBASE, true> {
-    static PCUB_HD uint32_t run(double v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane) {
-#if DIAG_XSUB == 1
-        // no arithmetic: decisions = the frozen values (results are wrong; times the level's cost)
-        ub |= fv & (0xFull << UBASE);
-        return (uint32_t)(as_bits(v) & 1);
-#else
-        // the original M = 4 node, its M = 2 children deciding both leaves of a pair at once
-        const double w = xor_shfl_c<2>(v);
-        const bool lo = (lane & 2) == 0;
-        const double a = lo ? v : w, b = lo ? w : v;
-        constexpr uint64_t HM = 3ull;
-        const int pos = lane & 1;
-        uint32_t ym, yp;
-        if (all_frozen<2>(fm, UBASE)) {
-            ym = frozen_local<1, 2>(fv >> UBASE, pos) & 1u;
-            ub |= fv & (HM << UBASE);
-        } else {
-            ym = XSub<2, UBASE, true>::run(op_f(a, b), ub, fm, fv, lane);
-        }
-        if (all_frozen<2>(fm, UBASE + 2)) {
-            yp = frozen_local<1, 2>(fv >> (UBASE + 2), pos) & 1u;
-            ub |= fv & (HM << (UBASE + 2));
-        } else {
-            yp = XSub<2, UBASE + 2, true>::run(op_g(a, b, ym), ub, fm, fv, lane);
-        }
-        return lo ? (ym ^ yp) : yp;
-#endif
-    }
-};
-}  // namespace pcub
-#endif
+
 
 namespace {
 
@@ -62,7 +27,7 @@ struct Acc {
 
 __device__ __forceinline__ unsigned long long now() { return __builtin_amdgcn_s_memtime(); }
 
-template <int S, int G, int PF, int SP = 0, bool HSP = false, int PF1 = -1>
+template <int S, int G, int PF, int PF1 = -1>
 __device__ void decode_timed(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
                              uint32_t* ylds, long long ystride, double* hl, Acc& T) {
     constexpr bool LDS = false, YL = true, HL = true, CR = false;
@@ -70,7 +35,7 @@ __device__ void decode_timed(const BinArgs& A, long long cw, int j, int lane, lo
     constexpr int SR = 2 * S;
     constexpr int s = 6;
     constexpr int g = (G == 4) ? 2 : 3;
-    using W = SubWin<SR, G, SP>;
+    using W = SubWin<SR, G>;
     constexpr int NW = W::NW;
     constexpr int RR = 2;
     constexpr bool NS = false;
@@ -178,7 +143,7 @@ __device__ void decode_timed(const BinArgs& A, long long cw, int j, int lane, lo
             T.fk[k & 3] += t1 - t0;
             t0 = t1;
             if (e0 == D) y = hl_frozen<S, G>(ub, fv, j);
-            else y = hl_run<S, G, SP, HSP>(hl, v, ub, fm, fv, lane);
+            else y = hl_run<S, G>(hl, v, ub, fm, fv, lane);
             t1 = now();
             T.hl += t1 - t0;
             T.hk[k & 3] += t1 - t0;
@@ -225,7 +190,7 @@ __device__ void decode_timed(const BinArgs& A, long long cw, int j, int lane, lo
     T.rest += now() - t0;
 }
 
-template <int SP, bool HSP, int PF1>
+template <int PF1>
 __global__ __launch_bounds__(kBinBlock, 2) void k_timed(BinArgs A, unsigned long long* out) {
     extern __shared__ double2 lds_last[];
     constexpr int S = 32, G = 4;
@@ -239,7 +204,7 @@ __global__ __launch_bounds__(kBinBlock, 2) void k_timed(BinArgs A, unsigned long
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_timed<S, G, 2, SP, HSP, PF1>(A, valid ? cw : A.B - 1, j, lane, slot, valid,
+        decode_timed<S, G, 2, PF1>(A, valid ? cw : A.B - 1, j, lane, slot, valid,
                                        (uint32_t*)(lds_last + LDS2) + threadIdx.x, kBinBlock,
                                        (double*)lds_last + threadIdx.x, T);
     }
@@ -257,7 +222,7 @@ __global__ __launch_bounds__(kBinBlock, 2) void k_timed(BinArgs A, unsigned long
 }
 
 // the library's decode_codeword, variant 26's shape with prefetch distances PF / PF1
-template <int PF, int PF1, int SP>
+template <int PF, int PF1>
 __global__ __launch_bounds__(kBinBlock, 2) void k_real(BinArgs A, unsigned long long*) {
     extern __shared__ double2 lds_last[];
     constexpr int S = 32, G = 4;
@@ -270,7 +235,7 @@ __global__ __launch_bounds__(kBinBlock, 2) void k_real(BinArgs A, unsigned long 
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_codeword<S, G, false, 1, true, true, PF, false, SP, false, PF1>(
+        decode_codeword<S, G, false, 1, true, true, PF, false, PF1>(
             A, valid ? cw : A.B - 1, j, lane, slot, valid, Lvl{nullptr, 0}, (uint32_t*)(lds_last + LDS2) + threadIdx.x,
             kBinBlock, (double*)lds_last + threadIdx.x);
     }
@@ -423,19 +388,15 @@ int main(int argc, char** argv) {
         bool stamped;
     };
     const Cfg cfgs[] = {
-        {"v26 (PF 2)", k_real<2, -1, 0>, false},
-#if defined(DIAG_XSUB)
-        {DIAG_XSUB == 1 ? "XSub<4> stubbed (wrong results)" : "leaf pairs without a branch", k_real<2, -1, 1>, false},
-#else
-        {"stamped v26", k_timed<0, false, -1>, true},
-#endif
+        {"v26 (PF 2)", k_real<2, -1>, false},
+        {"stamped v26", k_timed<-1>, true},
     };
     for (int i = 0; i < (int)(sizeof(cfgs) / sizeof(cfgs[0])); ++i)
         if (only < 0 || only == i) run(cfgs[i].name, cfgs[i].k, cfgs[i].stamped, A, lds, grid, dout, reps);
     // the same codewords with the root in [B/16][N][16] tiles (one wave's 16 codewords contiguous)
     hipLaunchKernelGGL(k_inputs, dim3((unsigned)((B * N + 255) / 256)), dim3(256), 0, 0, xy, B * N, sigma2, B, N, 16);
     A.tile = 16;
-    run("v26, root in 16-codeword tiles", k_real<2, -1, 0>, false, A, lds, grid, dout, reps);
-    run("stamped, tiles", k_timed<0, false, -1>, true, A, lds, grid, dout, 2);
+    run("v26, root in 16-codeword tiles", k_real<2, -1>, false, A, lds, grid, dout, reps);
+    run("stamped, tiles", k_timed<-1>, true, A, lds, grid, dout, 2);
     return 0;
 }

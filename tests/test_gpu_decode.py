@@ -9,7 +9,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 BIN_SETS = ["bsc_n64", "awgn_n1024", "awgn_n4096", "awgn_n256_lowsnr"]
-NVAR = 38  # kernel variants (sc_bin_kern.h); 24-30, 32-37 keep the re-encoded bits in LDS, 26-28, 30-37 split their last level (LDS + registers), 33-37 speculate the plus transforms
+NVAR = 33  # kernel variants (sc_bin_kern.h); 24-30 and 32 keep the re-encoded bits in LDS, 26-28 and 30-32 split their last level (LDS + registers)
 
 
 def _xy(g):

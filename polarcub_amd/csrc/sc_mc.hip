@@ -14,9 +14,6 @@
 // driver (coding.encodeDecodeSimulation), which replays the reference's RNGs.
 #include <hip/hip_runtime.h>
 
-#include <map>
-#include <mutex>
-
 #include "polarcub_sc.h"
 #include "sc_common.h"
 
@@ -166,17 +163,22 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_
 // no SC decision depends on a row's positive scale), as compact values (+r: (1, r), -r: (r, 1);
 // COMPACT, [N][B] doubles) or as the pairs they stand for ([N][B][2]).  BI-AWGN: the likelihood
 // ratio p0 / p1 = exp(2y / sigma^2), so the row is (1, exp(-2y/s2)) for y >= 0, else
-// (exp(2y/s2), 1); BSC: makeBSC's row normalised (norm_pack).  Same Philox draws as k_mc_channel.
-__device__ __forceinline__ double awgn_norm(const McArgs& A, uint32_t xb, double z) {
-    const double y = (xb ? -1.0 : 1.0) + A.sigma * z;
-    const double l = y * A.inv2s2 * 4.0;  // 2 y / sigma^2
-    const double r = exp(-__builtin_fabs(l));
-    return l >= 0.0 ? r : -r;
-}
+// (exp(2y/s2), 1); BSC: makeBSC's row normalised (norm_pack).
+//
+// Draws (round 4): elements 4j..4j+3 of codeword g take the four words of Philox counter
+// (g, kStreamChannel, j) as 32-bit uniforms u = (r + 1) 2^-32 in (0, 1]: BI-AWGN pairs them into
+// two f32 Box-Muller transforms (|z| <= 6.66 at u = 2^-32) and forms y, 2y/s2 and exp(-|2y/s2|)
+// in f32, stored as the f64 row value; BSC flips where u <= p.  The noise is a simulation draw,
+// not a reference value: f32 rounds each row to a relative 6e-8, far below anything a frame-error
+// rate resolves, and the decode's arithmetic on the stored rows is the reference's in f64
+// (test_gpu_fer.py holds the FER to the reference's own runs).
+__device__ __forceinline__ float u01f(uint32_t r) { return ((float)r + 1.0f) * 2.3283064365386963e-10f; }
 
-__device__ __forceinline__ double bsc_norm(const McArgs& A, uint32_t xb, double u) {
-    const double2 o = bsc_pair(A, xb, u);
-    return norm_pack(o.x, o.y);
+__device__ __forceinline__ double awgn_normf(const McArgs& A, uint32_t xb, float z) {
+    const float y = (xb ? -1.0f : 1.0f) + (float)A.sigma * z;
+    const float l = y * (float)(A.inv2s2 * 4.0);  // 2 y / sigma^2
+    const float r = expf(-__builtin_fabsf(l));
+    return l >= 0.0f ? (double)r : -(double)r;
 }
 
 __device__ __forceinline__ void put_norm(double* out, long long at, double c, bool compact) {
@@ -194,25 +196,35 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel_norm(McArgs A, const ui
     if (b >= A.B) return;
     const uint64_t g = (uint64_t)(A.offset + b);
     const long long N = 1LL << A.n;
-    const long long pairs = (N + 1) / 2;
-    for (long long j = blockIdx.y; j < pairs; j += gridDim.y) {
-        const long long i0 = 2 * j;
-        const uint32_t xw = x[(i0 >> 5) * A.B + b] >> (i0 & 31);
+    const long long quads = (N + 3) / 4;
+    const long long base = row_at(A, 0, b), stride = A.tile > 0 ? (long long)A.tile : A.B;
+    const float pf = (float)A.param;
+    for (long long j = blockIdx.y; j < quads; j += gridDim.y) {
+        const long long i0 = 4 * j;
+        const uint32_t xw = x[(i0 >> 5) * A.B + b] >> (i0 & 31);  // bits i0..i0+3 (one word: i0 % 4 == 0)
         const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)j, (uint32_t)A.seed,
                             (uint32_t)(A.seed >> 32));
-        const double u0 = u01(r.v[0], r.v[1]), u1 = u01(r.v[2], r.v[3]);
-        double c0, c1;
+        double c[4];
         if (A.channel == 0) {
-            double z0, z1;
-            box_muller(u0, u1, z0, z1);
-            c0 = awgn_norm(A, xw & 1u, z0);
-            c1 = awgn_norm(A, (xw >> 1) & 1u, z1);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float rad = sqrtf(-2.0f * logf(u01f(r.v[2 * h])));
+                float sn, cs;
+                sincospif(2.0f * u01f(r.v[2 * h + 1]), &sn, &cs);
+                c[2 * h] = awgn_normf(A, (xw >> (2 * h)) & 1u, rad * cs);
+                c[2 * h + 1] = awgn_normf(A, (xw >> (2 * h + 1)) & 1u, rad * sn);
+            }
         } else {
-            c0 = bsc_norm(A, xw & 1u, u0);
-            c1 = bsc_norm(A, (xw >> 1) & 1u, u1);
+            const double hi = 0.5 * (1.0 - A.param), lo = 0.5 * A.param;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t yb = ((xw >> k) & 1u) ^ (u01f(r.v[k]) <= pf ? 1u : 0u);
+                c[k] = yb ? norm_pack(lo, hi) : norm_pack(hi, lo);
+            }
         }
-        put_norm(out, row_at(A, i0, b), c0, COMPACT);
-        if (i0 + 1 < N) put_norm(out, row_at(A, i0 + 1, b), c1, COMPACT);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i0 + k < N) put_norm(out, base + (i0 + k) * stride, c[k], COMPACT);
     }
 }
 
@@ -368,9 +380,9 @@ extern "C" int pcub_mc_channel_norm_tiled(uint64_t seed, int64_t offset, int64_t
         A.inv2s2 = 1.0 / (2.0 * param);
     }
     const long long gx = (B + kMcBlock - 1) / kMcBlock;
-    const long long pairs = (((long long)1 << log2N) + 1) / 2;
+    const long long quads = (((long long)1 << log2N) + 3) / 4;
     long long gy = (16384 + gx - 1) / gx;
-    if (gy > pairs) gy = pairs;
+    if (gy > quads) gy = quads;
     if (gy > 65535) gy = 65535;
     if (gx > 0x7fffffffLL) return PCUB_EINVAL;
     if (compact)
@@ -456,10 +468,13 @@ namespace {
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// Two generation slots (information words, compact channel rows), so the generation of chunk i+1
-// on a side stream overlaps the decode of chunk i on the caller's; one x and one decision buffer.
+// One generation slot (information words, channel rows), the codewords x and the decisions.  The
+// chunks run back to back on the caller's stream: round 3 generated chunk i+1 on a side stream while
+// chunk i decoded, and once the channel kernel got cheap that overlap measured slower than none
+// (C2, 2^20 codewords in chunks of 2^18: 56.5 M cw/s overlapped, 65.3 M serial, median of 5;
+// the decode holds the register file and the concurrent generation only takes its CUs).
 struct McLayout {
-    size_t info[2], x, xy[2], dec, dws, total;
+    size_t info, x, xy, dec, dws, total;
 };
 
 // the compact-root decode exists for the variant this code length runs (sc_bin.hip); otherwise the
@@ -479,31 +494,14 @@ McLayout mc_layout(int64_t chunk, int32_t log2N, int32_t K) {
     const size_t cp = (size_t)((chunk + T - 1) / T) * T;  // the chunk padded to whole tiles
     const size_t iw = (size_t)((K + 31) / 32 > 0 ? (K + 31) / 32 : 1);
     const size_t nw = (N + 31) / 32;
-    L.info[0] = 0;
-    L.info[1] = L.info[0] + align256(iw * chunk * 4);
-    L.x = L.info[1] + align256(iw * chunk * 4);
-    L.xy[0] = L.x + align256(nw * chunk * 4);
-    L.xy[1] = L.xy[0] + align256(N * cp * row);
-    L.dec = L.xy[1] + align256(N * cp * row);
+    L.info = 0;
+    L.x = L.info + align256(iw * chunk * 4);
+    L.xy = L.x + align256(nw * chunk * 4);
+    L.dec = L.xy + align256(N * cp * row);
     L.dws = L.dec + align256(iw * chunk * 4);
     L.total = L.dws + align256(mc_compact(log2N) ? pcub_sc_decode_bin_compact_workspace(chunk, log2N)
                                                  : pcub_sc_decode_bin_workspace(chunk, log2N));
     return L;
-}
-
-// the side stream of each device (created on first use, kept for the process)
-hipStream_t gen_stream() {
-    static std::mutex mu;
-    static std::map<int, hipStream_t> streams;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = streams.find(dev);
-    if (it != streams.end()) return it->second;
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    streams[dev] = s;
-    return s;
 }
 
 }  // namespace
@@ -526,68 +524,26 @@ extern "C" int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int
     uint32_t* x = (uint32_t*)(ws + L.x);
     uint32_t* dec = (uint32_t*)(ws + L.dec);
     const hipStream_t ms = (hipStream_t)stream;
-    const int64_t nchunk = count == 0 ? 0 : (count + chunk - 1) / chunk;
-    // chunk i's generation (info -> encode -> channel rows into slot i % 2) runs on the side stream
-    // and overlaps chunk i-1's decode on the caller's stream; slot reuse waits for the decode and
-    // the counting of chunk i-2.  One chunk: everything on the caller's stream.
-    const hipStream_t gs = nchunk > 1 ? gen_stream() : ms;
-    if (nchunk > 1 && !gs) return (int)hipErrorInvalidResourceHandle;  // (ms may be the null stream)
-    hipEvent_t start = nullptr, ready[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
+    uint32_t* info = (uint32_t*)(ws + L.info);
+    double* xy = (double*)(ws + L.xy);
     int rc = 0;
-    auto mk = [&](hipEvent_t* e) {
-        if (!rc) rc = (int)hipEventCreateWithFlags(e, hipEventDisableTiming);
-    };
-    if (gs != ms) {
-        mk(&start);
-        for (int i = 0; i < 2; ++i) {
-            mk(&ready[i]);
-            mk(&freed[i]);
-        }
-        if (!rc) rc = (int)hipEventRecord(start, ms);  // the caller's earlier work first
-        if (!rc) rc = (int)hipStreamWaitEvent(gs, start, 0);
-    }
-    auto gen = [&](int64_t i) -> int {
-        const int64_t c0 = i * chunk, B = (count - c0) < chunk ? (count - c0) : chunk;
-        const int k = (int)(i & 1);
-        uint32_t* info = (uint32_t*)(ws + L.info[k]);
-        double* xy = (double*)(ws + L.xy[k]);
-        int r;
-        if (gs != ms && i >= 2 && (r = (int)hipStreamWaitEvent(gs, freed[k], 0))) return r;
-        if (K > 0 && (r = pcub_mc_info(seed, offset + c0, B, K, info, gs))) return r;
-        if ((r = pcub_polar_encode_bin(info, B, log2N, frozen_mask, frozen_val, K, x, gs))) return r;
+    for (int64_t c0 = 0; !rc && c0 < count; c0 += chunk) {
+        const int64_t B = (count - c0) < chunk ? (count - c0) : chunk;
+        if (K > 0 && (rc = pcub_mc_info(seed, offset + c0, B, K, info, ms))) break;
+        if ((rc = pcub_polar_encode_bin(info, B, log2N, frozen_mask, frozen_val, K, x, ms))) break;
         // normalised rows in compact form (8 bytes a position) into the compact-root decode, or as
         // pairs where this code length has no compact-root kernel
-        if ((r = pcub_mc_channel_norm_tiled(seed, offset + c0, B, log2N, channel, param, x, xy, compact ? 1 : 0, T,
-                                            gs)))
-            return r;
-        if (gs != ms && (r = (int)hipEventRecord(ready[k], gs))) return r;
-        return 0;
-    };
-    for (int64_t i = 0; !rc && i < nchunk; ++i) {
-        const int64_t c0 = i * chunk, B = (count - c0) < chunk ? (count - c0) : chunk;
-        const int k = (int)(i & 1);
-        if (i == 0) rc = gen(0);
-        if (!rc && i + 1 < nchunk) rc = gen(i + 1);  // enqueued before this chunk's decode
-        if (rc) break;
-        if (gs != ms && (rc = (int)hipStreamWaitEvent(ms, ready[k], 0))) break;
+        if ((rc = pcub_mc_channel_norm_tiled(seed, offset + c0, B, log2N, channel, param, x, xy, compact ? 1 : 0, T,
+                                             ms)))
+            break;
         if (compact)
-            rc = pcub_sc_decode_bin_compact_tiled((const double*)(ws + L.xy[k]), B, log2N, T, frozen_mask, frozen_val, K,
-                                                  dec, nullptr, nullptr, ws + L.dws, L.total - L.dws, ms);
+            rc = pcub_sc_decode_bin_compact_tiled(xy, B, log2N, T, frozen_mask, frozen_val, K, dec, nullptr, nullptr,
+                                                  ws + L.dws, L.total - L.dws, ms);
         else
-            rc = pcub_sc_decode_bin_tiled((const double*)(ws + L.xy[k]), B, log2N, T, frozen_mask, frozen_val, K, dec,
-                                          nullptr, nullptr, ws + L.dws, L.total - L.dws, ms);
+            rc = pcub_sc_decode_bin_tiled(xy, B, log2N, T, frozen_mask, frozen_val, K, dec, nullptr, nullptr,
+                                          ws + L.dws, L.total - L.dws, ms);
         if (rc) break;
-        if ((rc = pcub_mc_count_errors(dec, (const uint32_t*)(ws + L.info[k]), B, K, counters, ms))) break;
-        if (gs != ms && (rc = (int)hipEventRecord(freed[k], ms))) break;
+        rc = pcub_mc_count_errors(dec, info, B, K, counters, ms);
     }
-    if (gs != ms && rc) {  // nothing of this call may still run on the side stream after it returns
-        hipEvent_t done = nullptr;
-        if (hipEventCreateWithFlags(&done, hipEventDisableTiming) == hipSuccess) {
-            if (hipEventRecord(done, gs) == hipSuccess) (void)hipStreamWaitEvent(ms, done, 0);
-            (void)hipEventDestroy(done);
-        }
-    }
-    for (hipEvent_t e : {start, ready[0], ready[1], freed[0], freed[1]})
-        if (e) (void)hipEventDestroy(e);
     return rc;
 }

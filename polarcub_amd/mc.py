@@ -149,7 +149,8 @@ def philox_batch(code, seed, offset, B, channel, param, tile=0):
 
 def philox_norm_batch(code, seed, offset, B, channel, param, compact=True):
     """Information words and the normalised channel rows of global codewords [offset, offset + B)
-    (the same draws as philox_batch, each row divided by its larger entry; pcub_mc_channel_norm):
+    (pcub_mc_channel_norm: four elements a Philox counter, f32 row arithmetic, each row divided by its
+    larger entry — the channel law of philox_batch, not its draws):
     compact [N, B] float64, or the pairs they stand for [N, B, 2]."""
     from . import _lib
     L = _lib.lib()

@@ -113,7 +113,8 @@ int pcub_polar_encode_bin(const uint32_t* info_words, int64_t B, int32_t log2N, 
  * Guardbands.py:47-93) builds from each received word.
  *   rx          [B][stride] u8 received symbols (0/1), rx_len[b] <= stride of them valid
  *   n, n0       code length 2^n, 2^n0 inputs per trellis; supported (decode):
- *               1 <= n0 <= 4, 1 <= n - n0 <= 8 (decode and leaf export)
+ *               1 <= n0 <= 4, 1 <= n - n0 <= 8 (decode and leaf export), and n0 = 4 with
+ *               n - n0 = 9, 10 without ones (decode; main_deletion's n = 13, 14)
  *               (pcub_sc_deletion_supported / pcub_sc_leaf_deletion_supported)
  *   ones        numberOfOnesToAddAtBothEndsOfGuardbands, 0 <= ones <= 3
  *   pd          deletion probability the trellises are built with
@@ -149,12 +150,12 @@ int pcub_sc_leaf_deletion(const uint8_t* rx, const int32_t* rx_len, int64_t B, i
  * (DESIGN 3.2).  pcub_sc_deletion_table_bytes(n0) is its size (0: no table for n0);
  * pcub_sc_deletion_build_table fills it on the stream (8-byte aligned device memory).
  * The _tab twins of the two deletion entry points read it when n0 = 2 or 3 and ones = 0 and the
- * table was built for the same pd (its stamp); otherwise, or with table = NULL, they decode
+ * table was built for the same n0 and pd (its header); otherwise, or with table = NULL, they decode
  * as the plain entry points (n0 = 2 then builds its table per workgroup).  Decisions are
  * identical either way.  The table must stay allocated and unmodified while decodes that read it
- * are in flight (ordinary stream rules: build and decode on one stream, or synchronise); the
- * library remembers (pointer, pd) of the tables it built (the last 64) and runs the table-driven
- * layout from a table only on those. */
+ * are in flight (ordinary stream rules: build and decode on one stream, or synchronise).  Every
+ * kernel checks the table's header (magic, n0, pd) on the device before reading it; a rejected
+ * table sends the batch to the table-less path. */
 int64_t pcub_sc_deletion_table_bytes(int32_t n0);
 /* Diagnostics: allow (1, the default) or forbid (0) the table-driven layout, 16 lanes per codeword
  * (DESIGN 3.2); returns the previous setting.  Decisions are identical either way. */
@@ -262,8 +263,9 @@ int pcub_sc_decode_bin_compact_tiled(const double* xc, int64_t B, int32_t log2N,
  *   pcub_mc_channel  codeword bits [ceil(N/32)][B] -> joint pairs [N][B][2] f64;
  *                    channel 0 = BI-AWGN (param = sigma^2, BPSK 0 -> +1),
  *                    channel 1 = BSC (param = p, makeBSC's table)
- *   pcub_mc_channel_norm  the same draws as normalised rows (each divided by its larger entry:
- *                    the same channel law), compact ([N][B] f64, compact != 0) or as pairs
+ *   pcub_mc_channel_norm  normalised rows (each divided by its larger entry: the same channel law;
+ *                    four elements a Philox counter, the row arithmetic in f32), compact
+ *                    ([N][B] f64, compact != 0) or as pairs
  *   pcub_mc_count_errors  counters[0] += B, [1] += frame errors, [2] += bit errors
  *   pcub_mc_run_bin  info -> encode -> channel (normalised, compact) -> decode -> count for codewords
  *                    [offset, offset + count), chunk codewords at a time; counters
@@ -304,6 +306,29 @@ int pcub_mc_deletion(uint64_t seed, int64_t offset, int64_t B, int32_t log2N, co
 int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int32_t log2N, int32_t channel, double param,
                     const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K, int64_t chunk,
                     uint64_t* counters, void* workspace, size_t workspace_bytes, void* stream);
+
+/* mc_run for the q-ary and deletion workloads: the chained generators above, the decode and the
+ * counters for codewords [offset, offset + count), chunk at a time, on the stream.  counters
+ * (device u64[4], the caller zeroes them) accumulate [0] codewords, [1] frame errors, [2] symbol
+ * (q-ary) or information-bit (deletion) errors.
+ *   pcub_mc_run_qary      info (pcub_mc_info_qary) -> pcub_polar_encode_qary -> QSC(p) rows in the
+ *                         decode's tiles -> pcub_sc_decode_qary_tiled -> symbol errors
+ *                         (QaryPolarEncoderDecoder.py:935-982's trial loop)
+ *   pcub_mc_run_deletion  info -> pcub_polar_encode_bin -> pcub_mc_deletion (template tmpl of W
+ *                         entries, channel pd) -> pcub_sc_decode_deletion_tab (stride W, trellises
+ *                         built with the same pd; table as there, may be NULL) -> bit errors
+ *                         (main_deletion.py:142-146's trial loop)
+ * Workspaces: pcub_mc_run_qary_workspace(chunk, log2N, q, K), pcub_mc_run_deletion_workspace(chunk,
+ * n, W, K) bytes. */
+size_t pcub_mc_run_qary_workspace(int64_t chunk, int32_t log2N, int32_t q, int32_t K);
+int pcub_mc_run_qary(uint64_t seed, int64_t offset, int64_t count, int32_t log2N, int32_t q, double p,
+                     const uint8_t* frozen, int32_t K, int64_t chunk, uint64_t* counters, void* workspace,
+                     size_t workspace_bytes, void* stream);
+size_t pcub_mc_run_deletion_workspace(int64_t chunk, int32_t n, int32_t W, int32_t K);
+int pcub_mc_run_deletion(uint64_t seed, int64_t offset, int64_t count, int32_t n, int32_t n0, const int32_t* tmpl,
+                         int32_t W, int32_t ones, double pd, const uint32_t* frozen_mask, const uint32_t* frozen_val,
+                         int32_t K, const double* table, int64_t chunk, uint64_t* counters, void* workspace,
+                         size_t workspace_bytes, void* stream);
 
 /* [B][nbits] u8 (0/1) -> ceil(nbits/32) x B words, and back. */
 int pcub_pack_bits(const uint8_t* bits, int64_t B, int32_t nbits, uint32_t* words, void* stream);

@@ -171,6 +171,17 @@ def lib():
     L.pcub_mc_run_bin.restype = ctypes.c_int
     L.pcub_mc_run_bin.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _c_void_p, _i32, _i64,
                                   _c_void_p, _c_void_p, ctypes.c_size_t, _c_void_p]
+    L.pcub_mc_run_qary_workspace.restype = ctypes.c_size_t
+    L.pcub_mc_run_qary_workspace.argtypes = [_i64, _i32, _i32, _i32]
+    L.pcub_mc_run_qary.restype = ctypes.c_int
+    L.pcub_mc_run_qary.argtypes = [_u64, _i64, _i64, _i32, _i32, ctypes.c_double, _c_void_p, _i32, _i64, _c_void_p,
+                                   _c_void_p, ctypes.c_size_t, _c_void_p]
+    L.pcub_mc_run_deletion_workspace.restype = ctypes.c_size_t
+    L.pcub_mc_run_deletion_workspace.argtypes = [_i64, _i32, _i32, _i32]
+    L.pcub_mc_run_deletion.restype = ctypes.c_int
+    L.pcub_mc_run_deletion.argtypes = [_u64, _i64, _i64, _i32, _i32, _c_void_p, _i32, _i32, ctypes.c_double,
+                                       _c_void_p, _c_void_p, _i32, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                       ctypes.c_size_t, _c_void_p]
     if L.pcub_abi_version() != ABI_VERSION:
         raise ImportError("libpolarcub_hip.so ABI mismatch; rebuild with python -m polarcub_amd.build --force")
     _lib = L
@@ -190,7 +201,8 @@ EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_b
            "pcub_sc_deletion_build_table", "pcub_sc_decode_deletion_tab", "pcub_sc_leaf_deletion_tab",
            "pcub_sc_set_deletion_dense", "pcub_sc_deletion_dense_layout", "pcub_sc_bin_tile", "pcub_sc_decode_bin_tiled",
            "pcub_sc_decode_bin_compact_tiled", "pcub_mc_channel_tiled", "pcub_mc_channel_norm_tiled",
-           "pcub_mc_channel_qsc_tiled", "pcub_sc_qary_tile", "pcub_sc_decode_qary_tiled"]
+           "pcub_mc_channel_qsc_tiled", "pcub_sc_qary_tile", "pcub_sc_decode_qary_tiled",
+           "pcub_mc_run_qary_workspace", "pcub_mc_run_qary", "pcub_mc_run_deletion_workspace", "pcub_mc_run_deletion"]
 
 
 def check(rc, what):

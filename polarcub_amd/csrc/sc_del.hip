@@ -23,6 +23,9 @@ using namespace pcub;
 namespace {
 
 constexpr int kMaxOnes = 3;
+// received row stride: a segment's positions are relative to its start (16-bit vertex positions
+// in trellis_body.h), the row index itself is an int
+constexpr int kMaxStride = 1 << 24;
 
 std::atomic<int> g_dense{1};  // the table-driven layout allowed (pcub_sc_set_deletion_dense)
 
@@ -89,6 +92,7 @@ __global__ __launch_bounds__(256) void k_del_n02_table(double pd, double* tab) {
 DelKern del_kernel(int n0, int tb, bool exp, int ones) {
     if (ones < 0 || ones > kMaxOnes) return nullptr;
     const int oc = ones > 0 ? kMaxOnes : 0;
+    if (tb > 8) return n0 == 4 && !exp && oc == 0 ? del_kernel_n4_wide(tb) : nullptr;
 #define PCUB_DEL_PICK(k) \
     case k: return exp ? del_kernel_n##k##_x(tb, oc) : oc == 0 ? del_kernel_n##k##_d0(tb) : del_kernel_n##k##_d3(tb);
     switch (n0) {
@@ -145,7 +149,7 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
                const uint32_t* frozen_val_cw, int32_t K, uint32_t* info_words, uint32_t* xhat_words, double* leaf,
                const double* table, void* stream) {
     const DelKern kern = del_kernel(n0, n - n0, exp, ones);
-    if (!kern || B < 0 || stride < 0 || stride > 32767 || !frozen_mask || (!frozen_val && !frozen_val_cw))
+    if (!kern || B < 0 || stride < 0 || stride > kMaxStride || !frozen_mask || (!frozen_val && !frozen_val_cw))
         return PCUB_EINVAL;
     if (K < 0 || K > (1 << n) || (!exp && K > 0 && !info_words) || (B > 0 && (!rx || !rx_len))) return PCUB_EINVAL;
     if (exp && !leaf) return PCUB_EINVAL;
@@ -179,7 +183,9 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
         if (rc) return rc;
     }
     DelKern k = dense ? del_kernel_dense(n0, n - n0, n0 == 2 && A.tab) : kern;
-    long long cpb = dense ? kDenseCPB : kDelBlock >> (n - n0);
+    // the general kernel's workgroup: 256 threads, or T for 512 / 1024 trellises (one codeword)
+    const int blk = dense ? kDelBlock : ((n - n0) > 8 ? 1 << (n - n0) : kDelBlock);
+    long long cpb = dense ? kDenseCPB : blk >> (n - n0);
     long long grid = (B + cpb - 1) / cpb;
     // bit-packed received words in LDS when the group's words fit in 32 KiB (always for
     // the 64-trellis shapes; very long padded rows of small codes parse from HBM)
@@ -188,8 +194,8 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     // n0 = 2 without ones (and the table-driven layout): each workgroup first builds or copies the
     // segment-state table, so the launch is persistent
     if (dense || (n0 == 2 && ones == 0)) grid = resident_grid(k, lds, grid);
-    if (grid * kDelBlock > 0xffffffffLL) return PCUB_EINVAL;  // 32-bit dispatch grid (work-items)
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kDelBlock), lds, (hipStream_t)stream, A);
+    if (grid * blk > 0xffffffffLL) return PCUB_EINVAL;  // 32-bit dispatch grid (work-items)
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(blk), lds, (hipStream_t)stream, A);
     int rc = (int)hipGetLastError();
     if (rc || !checked) return rc;
     // the gated fallback: the same batch without the table, on a resident grid (its workgroups read
@@ -257,7 +263,7 @@ extern "C" int pcub_sc_set_deletion_dense(int32_t on) {
 
 extern "C" int pcub_sc_deletion_dense_layout(int32_t n, int32_t n0, int32_t ones, int32_t stride, const double* table,
                                              double pd) {
-    return del_kernel(n0, n - n0, false, ones) != nullptr && stride >= 0 && stride <= 32767 &&
+    return del_kernel(n0, n - n0, false, ones) != nullptr && stride >= 0 && stride <= kMaxStride &&
            use_dense(n, n0, ones, stride, table);
 }
 

@@ -44,6 +44,12 @@ namespace pcub {
 
 constexpr int kDelBlock = 256;
 
+// Workgroup size of the general kernel for T trellises: 256 threads (256 / T codewords), or one
+// codeword of T = 512 / 1024 trellises per workgroup of T threads (main_deletion's n0 = n // 3 at
+// n = 13, 14: 2^4-input trellises, T = 2^(n - 4)).
+template <int T>
+constexpr int del_block() { return T > kDelBlock ? T : kDelBlock; }
+
 struct DelArgs {
     const uint8_t* rx;      // [B][stride] received symbols (0/1)
     const int32_t* rx_len;  // [B]
@@ -119,10 +125,12 @@ __device__ __attribute__((noinline)) uint32_t del_window(V4 x, uint64_t& ub, uin
     return SubV<4, 0, 16>::run(x.v, ub, fm, fv, lane);
 }
 
+// (bits of L values a lane: 64 at T = 1024)
 template <int L, int NWIN>
 struct DelWin {
-    static __device__ __forceinline__ uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm,
-                                                   const uint64_t* fv, int lane) {
+    using Bits = typename std::conditional<(L > 32), uint64_t, uint32_t>::type;
+    static __device__ __forceinline__ Bits run(const double* v, uint64_t* ub, const uint64_t* fm,
+                                               const uint64_t* fv, int lane) {
         if constexpr (NWIN == 1) {
             static_assert(L == 4, "one window = 4 values x 16 lanes");
             V4 x;
@@ -148,7 +156,7 @@ struct DelWin {
                 for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
                 yp = DelWin<H, HW>::run(c, ub + HW, fm + HW, fv + HW, lane);
             }
-            return (ym ^ yp) | (yp << H);
+            return (Bits)(ym ^ yp) | ((Bits)yp << H);
         }
     }
 };
@@ -157,7 +165,7 @@ struct DelWin {
 template <int T, bool EXP>
 struct DelCtx {
     static constexpr int NW = T > 64 ? T / 64 : 1;  // 64-bit windows of a memoryless subtree
-    static constexpr int CPB = kDelBlock / T;       // codewords per workgroup
+    static constexpr int CPB = del_block<T>() / T;  // codewords per workgroup
     static constexpr int GL = 16;                   // wave-0 lanes per codeword (T >= 64)
     static constexpr int LV = T >= 64 ? T / GL : 1;  // values per wave-0 lane (T >= 64)
     DelArgs A;  // by value: taking the kernel argument's address would force it to scratch
@@ -235,7 +243,7 @@ struct DelCtx {
                 uint64_t ubl[NW];
 #pragma unroll
                 for (int w = 0; w < NW; ++w) ubl[w] = 0;
-                uint32_t bits;
+                typename DelWin<LV, NW>::Bits bits;
                 if constexpr (NW == 1) bits = WinTree<LV, GL, NW>::run(vv, ubl, fm, fv, lane);
                 else bits = DelWin<LV, NW>::run(vv, ubl, fm, fv, lane);
 #pragma unroll
@@ -583,10 +591,10 @@ __device__ __forceinline__ uint32_t del_n02(const Base02& b, DelCtx<T, EXP>& cx)
 // symbols, not per 64).
 constexpr int kPackU = 16;
 
-template <int CPB>
+template <int CPB, int BLK = kDelBlock>
 __device__ __forceinline__ void pack_rows(const DelArgs& A, long long grp, uint32_t* rxb, int lane) {
     const int nch = (A.rw * 32 + 63) / 64;  // 64-symbol chunks per row
-    for (int gg = threadIdx.x >> 6; gg < CPB; gg += kDelBlock / 64) {
+    for (int gg = threadIdx.x >> 6; gg < CPB; gg += BLK / 64) {
         long long cg = grp * CPB + gg;
         cg = cg < A.B ? cg : A.B - 1;
         const uint8_t* row = A.rx + cg * (long long)A.stride;
@@ -613,7 +621,8 @@ template <int N0, int TB, bool EXP, int OC>
 __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint32_t* xs, const double* n02tab) {
     constexpr int L = 1 << N0;
     constexpr int T = 1 << TB;
-    constexpr int CPB = kDelBlock / T;       // codewords per workgroup
+    constexpr int BLK = del_block<T>();
+    constexpr int CPB = BLK / T;             // codewords per workgroup
     constexpr int NB = T * L;                // code length N
     constexpr int WPC = (NB + 31) / 32;      // x_hat words per codeword
     using Cap = DelCap<L, OC>;
@@ -624,7 +633,7 @@ __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint3
     const long long cw = grp * CPB + g;
     const bool valid = cw < A.B;
     const long long c = valid ? cw : A.B - 1;  // padding groups decode a duplicate, store nothing
-    for (int i = threadIdx.x; i < CPB * WPC; i += kDelBlock) xs[i] = 0;
+    for (int i = threadIdx.x; i < CPB * WPC; i += BLK) xs[i] = 0;
 
     // Received words, bit-packed into LDS (rw > 0, the launcher's choice when the
     // group's words fit): each wave packs whole codewords with coalesced byte loads
@@ -633,7 +642,7 @@ __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint3
     extern __shared__ uint32_t rxb[];
     const bool pk = A.rw > 0;
     if (pk) {
-        pack_rows<CPB>(A, grp, rxb, lane);
+        pack_rows<CPB, BLK>(A, grp, rxb, lane);
         __syncthreads();
     }
 
@@ -647,7 +656,7 @@ __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint3
     if (pk) segment_of_packed(pw, len, TB, t, s, m);
     else segment_of(bit, len, TB, t, s, m);
 
-    __shared__ double xv[(T >= 64 && !EXP) ? kDelBlock : 1];
+    __shared__ double xv[(T >= 64 && !EXP) ? BLK : 1];
     __shared__ unsigned long long xb[(T >= 64 && !EXP) ? DelCtx<T, EXP>::LV : 1],
         xub[(T >= 64 && !EXP) ? CPB * DelCtx<T, EXP>::NW : 1];
     __shared__ double xe[(T > 64 && EXP) ? 2 * kDelBlock : 1];
@@ -704,11 +713,13 @@ __device__ __forceinline__ void del_group(const DelArgs& A, long long grp, uint3
 }
 
 template <int N0, int TB, bool EXP, int OC>
-__global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
+__global__ __launch_bounds__(del_block<(1 << TB)>()) void k_sc_del(DelArgs A) {
     constexpr int T = 1 << TB;
-    constexpr int CPB = kDelBlock / T;                // codewords per workgroup
+    constexpr int BLK = del_block<T>();
+    constexpr int CPB = BLK / T;                      // codewords per workgroup
     constexpr int WPC = ((T << N0) + 31) / 32;        // x_hat words per codeword
-    static_assert(T <= kDelBlock, "at most one workgroup per codeword");
+    static_assert(T <= 1024, "at most one workgroup per codeword");
+    static_assert(!EXP || T <= kDelBlock, "export mode: at most 256 trellises");
     constexpr bool TAB = N0 == 2 && OC == 0;  // the n0 = 2 stage through the state table
     __shared__ uint32_t xs[CPB * WPC];
     __shared__ double n02tab[TAB ? kN02States * kN02Row : 1];
@@ -717,7 +728,7 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del(DelArgs A) {
     if (A.gate && *A.gate != A.gate_id) return;
     if constexpr (TAB) {
         // once per workgroup (the launch is persistent: a workgroup strides over codeword groups)
-        for (int i = threadIdx.x; i < kN02States * 5; i += kDelBlock)
+        for (int i = threadIdx.x; i < kN02States * 5; i += BLK)
             n02_table_entry(i / 5, i % 5, A.pd, n02tab + (i / 5) * kN02Row);
         __syncthreads();
     }
@@ -740,6 +751,9 @@ PCUB_DEL_TABLE(2)
 PCUB_DEL_TABLE(3)
 PCUB_DEL_TABLE(4)
 #undef PCUB_DEL_TABLE
+// 512 and 1024 trellises of 2^4 inputs (a workgroup of T threads per codeword; main_deletion's
+// n0 = n // 3 at n = 13, 14), decode without ones: sc_del_n4w.hip
+DelKern del_kernel_n4_wide(int tb);
 
 // Kernel tables, one per translation-unit group (decode without / with guard-band ones, export),
 // so the large n0 = 3, 4 instantiations compile in parallel.  T up to 256 (one workgroup) in

@@ -259,6 +259,37 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_count(const uint32_t* dec, cons
     }
 }
 
+// q-ary: counters[0] += B, [1] += frame errors, [2] += symbol errors over [K][B] u8 symbols
+__global__ __launch_bounds__(kMcBlock) void k_mc_count_sym(const uint8_t* dec, const uint8_t* sent, long long B, int K,
+                                                            unsigned long long* counters) {
+    __shared__ unsigned long long fe[kMcBlock / 64], se[kMcBlock / 64];
+    const long long b = (long long)blockIdx.x * kMcBlock + threadIdx.x;
+    unsigned long long f = 0, e = 0;
+    if (b < B) {
+        for (int k = 0; k < K; ++k) e += dec[(long long)k * B + b] != sent[(long long)k * B + b] ? 1ull : 0ull;
+        f = e ? 1ull : 0ull;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        f += __shfl_xor(f, o);
+        e += __shfl_xor(e, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        fe[threadIdx.x >> 6] = f;
+        se[threadIdx.x >> 6] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long tf = 0, ts = 0;
+        for (int i = 0; i < kMcBlock / 64; ++i) {
+            tf += fe[i];
+            ts += se[i];
+        }
+        atomicAdd(&counters[1], tf);
+        atomicAdd(&counters[2], ts);
+        if (blockIdx.x == 0) atomicAdd(&counters[0], (unsigned long long)B);
+    }
+}
+
 unsigned grid_of(long long work) { return (unsigned)((work + kMcBlock - 1) / kMcBlock); }
 
 // uniform symbol in [0, m) from 32 random bits (multiply-shift)
@@ -543,6 +574,128 @@ extern "C" int pcub_mc_run_bin(uint64_t seed, int64_t offset, int64_t count, int
             rc = pcub_sc_decode_bin_tiled(xy, B, log2N, T, frozen_mask, frozen_val, K, dec, nullptr, nullptr,
                                           ws + L.dws, L.total - L.dws, ms);
         if (rc) break;
+        rc = pcub_mc_count_errors(dec, info, B, K, counters, ms);
+    }
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// mc_run for the q-ary and deletion workloads (mc_run(cfg, seed, cw_offset, count) ->
+// counters): the same chunked, stream-ordered chain as pcub_mc_run_bin over the generators the
+// parity tests use, so a run's counters are what composing those calls counts.
+
+namespace {
+
+struct QLayout {
+    size_t info, x, xy, dec, dws, total;
+};
+
+QLayout q_layout(int64_t chunk, int32_t log2N, int32_t q, int32_t K) {
+    QLayout L;
+    const size_t N = (size_t)1 << log2N;
+    const int T = pcub_sc_qary_tile(q, log2N);
+    const size_t cp = (size_t)((chunk + T - 1) / T) * T;
+    const size_t kk = (size_t)(K > 0 ? K : 1);
+    L.info = 0;
+    L.x = L.info + align256(kk * chunk);
+    L.xy = L.x + align256(N * chunk);
+    L.dec = L.xy + align256(N * cp * q * 8);
+    L.dws = L.dec + align256(kk * chunk);
+    L.total = L.dws + align256(pcub_sc_decode_qary_workspace((int64_t)cp, log2N, q));
+    return L;
+}
+
+struct DLayout {
+    size_t info, x, rx, len, dec, total;
+};
+
+DLayout d_layout(int64_t chunk, int32_t n, int32_t W, int32_t K) {
+    DLayout L;
+    const size_t iw = (size_t)((K + 31) / 32 > 0 ? (K + 31) / 32 : 1);
+    const size_t nw = (((size_t)1 << n) + 31) / 32;
+    L.info = 0;
+    L.x = L.info + align256(iw * chunk * 4);
+    L.rx = L.x + align256(nw * chunk * 4);
+    L.len = L.rx + align256((size_t)W * chunk);
+    L.dec = L.len + align256((size_t)chunk * 4);
+    L.total = L.dec + align256(iw * chunk * 4);
+    return L;
+}
+
+}  // namespace
+
+extern "C" size_t pcub_mc_run_qary_workspace(int64_t chunk, int32_t log2N, int32_t q, int32_t K) {
+    if (chunk <= 0 || pcub_sc_qary_tile(q, log2N) <= 0 || K < 0 || K > (1 << log2N)) return 0;
+    return q_layout(chunk, log2N, q, K).total;
+}
+
+extern "C" int pcub_mc_run_qary(uint64_t seed, int64_t offset, int64_t count, int32_t log2N, int32_t q, double p,
+                                const uint8_t* frozen, int32_t K, int64_t chunk, uint64_t* counters, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+    if (count < 0 || offset < 0 || chunk <= 0 || !counters || !frozen) return PCUB_EINVAL;
+    const int T = pcub_sc_qary_tile(q, log2N);
+    if (T <= 0 || K < 0 || K > (1 << log2N) || !(p >= 0.0 && p <= 1.0)) return PCUB_EINVAL;
+    const QLayout L = q_layout(chunk, log2N, q, K);
+    if (!workspace || workspace_bytes < L.total) return PCUB_EINVAL;
+    char* ws = (char*)workspace;
+    uint8_t* info = (uint8_t*)(ws + L.info);
+    uint8_t* x = (uint8_t*)(ws + L.x);
+    double* xy = (double*)(ws + L.xy);
+    uint8_t* dec = (uint8_t*)(ws + L.dec);
+    const hipStream_t ms = (hipStream_t)stream;
+    int rc = 0;
+    for (int64_t c0 = 0; !rc && c0 < count; c0 += chunk) {
+        const int64_t B = (count - c0) < chunk ? (count - c0) : chunk;
+        if (K > 0 && (rc = pcub_mc_info_qary(seed, offset + c0, B, K, q, info, ms))) break;
+        if ((rc = pcub_polar_encode_qary(info, B, log2N, q, frozen, K, x, ms))) break;
+        if ((rc = pcub_mc_channel_qsc_tiled(seed, offset + c0, B, log2N, q, p, x, xy, T, ms))) break;
+        if ((rc = pcub_sc_decode_qary_tiled(xy, B, log2N, q, T, frozen, K, dec, nullptr, ws + L.dws, L.total - L.dws,
+                                            ms)))
+            break;
+        if (K == 0) {
+            hipLaunchKernelGGL(k_mc_count_sym, dim3(1), dim3(kMcBlock), 0, ms, dec, info, (long long)B, 0,
+                               (unsigned long long*)counters);
+        } else {
+            hipLaunchKernelGGL(k_mc_count_sym, dim3(grid_of(B)), dim3(kMcBlock), 0, ms, dec, info, (long long)B, (int)K,
+                               (unsigned long long*)counters);
+        }
+        rc = (int)hipGetLastError();
+    }
+    return rc;
+}
+
+extern "C" size_t pcub_mc_run_deletion_workspace(int64_t chunk, int32_t n, int32_t W, int32_t K) {
+    if (chunk <= 0 || n < 1 || n > 24 || W < 0 || K < 0 || K > (1 << n)) return 0;
+    return d_layout(chunk, n, W, K).total;
+}
+
+extern "C" int pcub_mc_run_deletion(uint64_t seed, int64_t offset, int64_t count, int32_t n, int32_t n0,
+                                    const int32_t* tmpl, int32_t W, int32_t ones, double pd,
+                                    const uint32_t* frozen_mask, const uint32_t* frozen_val, int32_t K,
+                                    const double* table, int64_t chunk, uint64_t* counters, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+    if (count < 0 || offset < 0 || chunk <= 0 || !counters || !frozen_mask || !frozen_val || !tmpl || W <= 0)
+        return PCUB_EINVAL;
+    if (!pcub_sc_deletion_supported(n, n0, ones) || K < 0 || K > (1 << n) || !(pd >= 0.0 && pd <= 1.0))
+        return PCUB_EINVAL;
+    const DLayout L = d_layout(chunk, n, W, K);
+    if (!workspace || workspace_bytes < L.total) return PCUB_EINVAL;
+    char* ws = (char*)workspace;
+    uint32_t* info = (uint32_t*)(ws + L.info);
+    uint32_t* x = (uint32_t*)(ws + L.x);
+    uint8_t* rx = (uint8_t*)(ws + L.rx);
+    int32_t* len = (int32_t*)(ws + L.len);
+    uint32_t* dec = (uint32_t*)(ws + L.dec);
+    const hipStream_t ms = (hipStream_t)stream;
+    int rc = 0;
+    for (int64_t c0 = 0; !rc && c0 < count; c0 += chunk) {
+        const int64_t B = (count - c0) < chunk ? (count - c0) : chunk;
+        if (K > 0 && (rc = pcub_mc_info(seed, offset + c0, B, K, info, ms))) break;
+        if ((rc = pcub_polar_encode_bin(info, B, n, frozen_mask, frozen_val, K, x, ms))) break;
+        if ((rc = pcub_mc_deletion(seed, offset + c0, B, n, tmpl, W, pd, x, rx, len, ms))) break;
+        if ((rc = pcub_sc_decode_deletion_tab(rx, len, B, W, n, n0, ones, pd, frozen_mask, frozen_val, K, dec, nullptr,
+                                              table, ms)))
+            break;
         rc = pcub_mc_count_errors(dec, info, B, K, counters, ms);
     }
     return rc;

@@ -56,10 +56,12 @@ PCUB_HD double fma_d(double a, double b, double c) { return __builtin_fma(a, b, 
 // tests/emu checks the fast path against division over random and edge inputs.
 template <int Q>
 PCUB_HD void q_div(QV<Q>& v, double t) {
+    // (bitwise & and |, not && and ||: the short-circuit form compiled to one exec-masked branch per
+    // component, ~20 scalar instructions a call)
     const double lo = t * 0x1p-800;
-    bool fast = t >= 0x1p-200 && t <= 0x1p+200;
+    bool fast = (t >= 0x1p-200) & (t <= 0x1p+200);
 #pragma unroll
-    for (int x = 0; x < Q; ++x) fast = fast && (v.p[x] == 0.0 || v.p[x] >= lo);
+    for (int x = 0; x < Q; ++x) fast = fast & ((v.p[x] == 0.0) | (v.p[x] >= lo));
     if (fast) {
         const double y = 1.0 / t;
 #pragma unroll

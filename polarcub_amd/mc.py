@@ -182,6 +182,44 @@ def run_bin(code, seed, offset, count, channel, param, chunk=1 << 18):
     return [int(v) for v in counters.tolist()]
 
 
+def run_qary(code, seed, offset, count, p, chunk=1 << 18):
+    """QaryPolarEncoderDecoder's QSC trial loop as one device pipeline (pcub_mc_run_qary: the
+    philox_qsc_batch generators, the tiled decode, symbol-error counting) over global codewords
+    [offset, offset + count); returns [codewords, frame errors, symbol errors, 0]."""
+    from . import _lib
+    L = _lib.lib()
+    chunk = int(max(1, min(chunk, count)))
+    need = int(L.pcub_mc_run_qary_workspace(chunk, code.n, code.q, code.K))
+    if need == 0:
+        raise ValueError("pcub_mc_run_qary: no decode kernel for q=%d N=%d" % (code.q, code.N))
+    ws = torch.empty(need, dtype=torch.uint8, device=code.device)
+    counters = torch.zeros(4, dtype=torch.int64, device=code.device)
+    _lib.check(L.pcub_mc_run_qary(int(seed), int(offset), int(count), code.n, code.q, float(p), sc._p(code.frozen_dev),
+                                  code.K, chunk, sc._p(counters), sc._p(ws), ws.numel(), sc._stream()),
+               "pcub_mc_run_qary")
+    return [int(v) for v in counters.tolist()]
+
+
+def run_deletion(code, seed, offset, count, n0, xi, pd, ones=0, table=None, chunk=1 << 18):
+    """main_deletion's trial loop as one device pipeline (pcub_mc_run_deletion: the
+    philox_deletion_batch generators, the deletion decode with trellises built for pd, bit-error
+    counting) over global codewords [offset, offset + count); returns [codewords, frame errors,
+    bit errors, 0]."""
+    from . import _lib
+    L = _lib.lib()
+    t = guard_template(code.n, n0, xi, ones, code.device)
+    W = int(t.numel())
+    chunk = int(max(1, min(chunk, count)))
+    need = int(L.pcub_mc_run_deletion_workspace(chunk, code.n, W, code.K))
+    ws = torch.empty(max(need, 16), dtype=torch.uint8, device=code.device)
+    counters = torch.zeros(4, dtype=torch.int64, device=code.device)
+    _lib.check(L.pcub_mc_run_deletion(int(seed), int(offset), int(count), code.n, int(n0), sc._p(t), W, int(ones),
+                                      float(pd), sc._p(code.fmask_dev), sc._p(code.fval_dev), code.K,
+                                      sc._p(table) if table is not None else None, chunk, sc._p(counters), sc._p(ws),
+                                      ws.numel(), sc._stream()), "pcub_mc_run_deletion")
+    return [int(v) for v in counters.tolist()]
+
+
 def philox_qsc_batch(code, seed, offset, B, p, tile=0):
     """q-ary information [K, B] u8 and QSC(p) joint rows [N, B, q] for global codewords
     [offset, offset + B) (pcub_mc_info_qary -> pcub_polar_encode_qary -> pcub_mc_channel_qsc);

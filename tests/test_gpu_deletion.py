@@ -84,6 +84,40 @@ def test_random_vs_oracle(sc, n0, n, ones):
         assert list(xhat[i]) == x_ref, (i, w)
 
 
+@pytest.mark.parametrize("n", [13, 14])
+def test_wide_shapes_vs_c_oracle(sc, n):
+    """main_deletion's n0 = n // 3 at n = 13, 14: 512 / 1024 trellises of 16 inputs, one codeword a
+    workgroup of T threads.  Channel outputs at pd 0.1 and 0.3, an empty, a one-symbol and an
+    all-zeros word and a random overlong one, random frozen set, against the C oracle
+    (oracle/trellis_oracle.c, pinned to the reference's goldens and the Python oracle)."""
+    from oracle import orc
+    n0 = 4
+    assert sc.deletion_supported(n, n0, 0)
+    N = 1 << n
+    rng = np.random.default_rng(77 + n)
+    prng = random.Random(n)
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    frozen[: N // 4] = 1
+    frozen[-(N // 8):] = 0
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    pd = 0.1
+    words = []
+    for t in range(3):
+        x = [int(b) for b in rng.integers(0, 2, N)]
+        cw = tro.add_guard_bands(x, n, n0, 0.1, 0)
+        words.append(tro.deletion_channel(cw, 0.1 if t < 2 else 0.3, prng))
+    words += [[], [1], [0] * 9, [int(b) for b in rng.integers(0, 2, 2 * N)]]
+    W = max(len(w) for w in words)
+    rx = np.zeros((len(words), W), np.uint8)
+    for i, w in enumerate(words):
+        rx[i, :len(w)] = w
+    ln = np.array([len(w) for w in words], np.int32)
+    info, xhat = _dec(sc, n, n0, pd, frozen, fval, rx, ln)
+    i_ref, x_ref = orc.decode_deletion(rx, ln, n, n0, pd, frozen, fval)
+    assert np.array_equal(info, i_ref)
+    assert np.array_equal(xhat, x_ref)
+
+
 def test_ragged_batches_match_single(sc):
     """A large batch (padding groups in the last workgroup) equals per-codeword results."""
     g = load_golden("deletion_n8")

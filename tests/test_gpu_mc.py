@@ -219,6 +219,43 @@ def test_deletion_sharded_counters_match_single_run(dcode):
     assert one == (a[0] + b[0], a[1] + b[1]) and one[0] > 0
 
 
+# -- mc_run for q-ary and deletion: the device pipelines count what the composed calls count -------
+
+def test_run_qary_matches_composed_pipeline(qcode):
+    """pcub_mc_run_qary over [off, off + B) in chunks = philox_qsc_batch -> QaryDecoder -> symbol
+    errors on the same codewords; sharding the range over two calls adds up."""
+    from polarcub_amd import mc, sc
+    B, off, p = 5000, 700, 0.11
+    got = mc.run_qary(qcode, 17, off, B, p, chunk=1536)
+    info, xy = mc.philox_qsc_batch(qcode, 17, off, B, p)
+    out = sc.QaryDecoder(qcode).decode_native(xy)[0]
+    fe, se = mc.error_counts(out.t(), info.t())
+    assert got[:3] == [B, fe, se] and fe > 0
+    a = mc.run_qary(qcode, 17, off, 2000, p)
+    b = mc.run_qary(qcode, 17, off + 2000, B - 2000, p)
+    assert [x + y for x, y in zip(a, b)] == got
+
+
+@pytest.mark.parametrize("n,n0,ones", [(8, 2, 0), (8, 2, 1), (10, 3, 0)])
+def test_run_deletion_matches_composed_pipeline(n, n0, ones):
+    """pcub_mc_run_deletion = philox_deletion_batch -> DeletionDecoder (table where it has one) ->
+    bit errors on the same codewords, for main_deletion's shapes and with guard-band ones."""
+    from polarcub_amd import construction, mc, sc
+    N = 1 << n
+    fr = construction.bhattacharyya_frozen(n, N // 4, 0.5)
+    code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(fr)[0].tolist()), 200, device="cuda")
+    dec = sc.DeletionDecoder(code, n0, 0.1, ones)
+    B, off = 3000, 123
+    tab = dec.table(code.device)
+    got = mc.run_deletion(code, 29, off, B, n0, 0.1, 0.1, ones, table=tab, chunk=1024)
+    info_w, rx, ln = mc.philox_deletion_batch(code, 29, off, B, n0, 0.1, 0.1, ones)
+    iw, _ = dec.decode_native(rx, ln)
+    fe, be = mc.error_counts(sc.unpack(iw, code.K), sc.unpack(info_w, code.K))
+    assert got[:3] == [B, fe, be] and fe > 0
+    if tab is not None:  # the table-less launch decides the same
+        assert mc.run_deletion(code, 29, off, B, n0, 0.1, 0.1, ones, table=None) == got
+
+
 # -- compact normalised rows: the end-to-end pipeline's format ------------------------------------
 
 @pytest.mark.parametrize("n", [4, 6, 8, 10, 11, 12])

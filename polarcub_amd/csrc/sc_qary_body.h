@@ -62,7 +62,9 @@ PCUB_HD void q_div(QV<Q>& v, double t) {
     bool fast = (t >= 0x1p-200) & (t <= 0x1p+200);
 #pragma unroll
     for (int x = 0; x < Q; ++x) fast = fast & ((v.p[x] == 0.0) | (v.p[x] >= lo));
-    if (fast) {
+    // A wave-uniform branch on the vote: when every lane is inside the guard (the common case) the
+    // fast path runs with no exec-mask bookkeeping; otherwise the per-lane choice.
+    auto fast_div = [&]() {
         const double y = 1.0 / t;
 #pragma unroll
         for (int x = 0; x < Q; ++x) {
@@ -70,18 +72,29 @@ PCUB_HD void q_div(QV<Q>& v, double t) {
             const double r = fma_d(-q0, t, v.p[x]);
             v.p[x] = fma_d(r, y, q0);
         }
-    } else {
+    };
+#ifdef __HIP_DEVICE_COMPILE__
+    if (__all(fast)) {
+        fast_div();
+        return;
+    }
+#endif
+    if (fast) {
+        fast_div();
+    } else if (t != 0.0) {
 #pragma unroll
         for (int x = 0; x < Q; ++x) v.p[x] = v.p[x] / t;
     }
 }
 
+// t = ((0 + p0) + p1) + ...; p[x] /= t unless t == 0 (then q_div leaves the vector, as the
+// reference's `if t != 0` does: the check sits in q_div's per-lane fallback, off the uniform path)
 template <int Q>
 PCUB_HD QV<Q> q_normalize(QV<Q> v) {
     double t = 0.0;
 #pragma unroll
     for (int x = 0; x < Q; ++x) t = t + v.p[x];
-    if (t != 0.0) q_div<Q>(v, t);
+    q_div<Q>(v, t);
     return v;
 }
 

@@ -89,12 +89,11 @@ PCUB_HD double op_f(double va, double vb) {
 // same orientation the division is skipped, which a select-based form measured 8 % slower for.)
 PCUB_HD double op_g(double va, double vb, uint32_t u) {
     const CV a = cv_load(va), b = cv_load(vb);
-    double q;
-    uint32_t s;
-    if ((a.s ^ u) == b.s) {
-        q = a.r * b.r;
-        s = b.s;
-    } else {
+    // the same-orientation result for every lane (one multiply), the opposite-orientation lanes
+    // overwrite it in a one-sided branch (no else region: two exec-mask instructions fewer)
+    double q = a.r * b.r;
+    uint32_t s = b.s;
+    if ((a.s ^ u) != b.s) {
         // a NaN lands in mn (a) or mx (b) and the quotient is NaN; 0/0 is the (0, 0) output
         const bool agt = a.r > b.r;
         const double mx = agt ? a.r : b.r;

@@ -50,6 +50,7 @@ KernFn variant_kernel(int v) {
 // falls back to 24 {32, 4, 3, NT, bits in LDS} (N = 4096: 13.3 M cw/s), then to 17
 constexpr int kDefaultVariant = 26;
 int g_variant = kDefaultVariant;
+int g_tiled_root = 1;  // pcub_sc_set_tiled_root
 int g_max_blocks = 0;  // workgroups per CU cap (0 = as many as fit)
 constexpr size_t kLdsPerCu = 160 * 1024;
 
@@ -161,6 +162,13 @@ extern "C" int pcub_sc_set_max_blocks_per_cu(int b) {
 }
 
 extern "C" int pcub_sc_default_variant(void) { return kDefaultVariant; }
+// Tuning hook (not part of the stable ABI): allow (1, the default) or forbid (0) the uniform-base
+// twins for rows in the wave's own tiles (bin_kernel_tiled_root); returns the previous setting.
+extern "C" int pcub_sc_set_tiled_root(int on) {
+    const int old = g_tiled_root;
+    g_tiled_root = on ? 1 : 0;
+    return old;
+}
 // the variant a decode of code length 2^log2N launches (the selected one, or its fallback)
 extern "C" int pcub_sc_variant_for(int32_t log2N) {
     if (log2N < 6 || log2N > 24) return PCUB_EINVAL;
@@ -236,7 +244,10 @@ int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N
     A.nslots = nslots;
     A.scratch = (double2*)slots;
     A.ybits = kVar[v].Y ? nullptr : (uint32_t*)(slots + (size_t)nslots * (Nv / 2 - bin_sr(v)) * sizeof(double2));
-    const BinKernFn kern = xc ? bin_kernel_compact(v) : variant_kernel(v);
+    // rows in the wave's own tiles: the uniform-base twin where one is instantiated
+    BinKernFn kern = nullptr;
+    if (g_tiled_root && tile == 64 / kVar[v].G) kern = bin_kernel_tiled_root(v, xc != nullptr);
+    if (!kern) kern = xc ? bin_kernel_compact(v) : variant_kernel(v);
     if (!kern) return PCUB_EINVAL;
     hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(kBlock), launch_lds(v, log2N), st, A);
     return (int)hipGetLastError();

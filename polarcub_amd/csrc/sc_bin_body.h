@@ -217,8 +217,9 @@ struct Lvl {
 // Source of a fused chain pass: the raw root (depth 0) or a stored level, plus
 // the partial sums of the first op's minus child when that op is a plus transform.
 struct Chain {
-    const double2* in;  // root: this lane's row 2*bitrev_{nv-1}(t) at in[2*bitrev(t)*B] (lane part folded in)
+    const double2* in;  // root: the wave's tile (uniform); this lane's rows at byte offset lin
     const double* inc;  // compact root (R == 3): the same rows, one double each
+    uint32_t lin;       // this lane's byte offset from in / inc (pairs: 16 B a row element, compact: 8)
     long long B;
     int nv;             // log2 of the virtual (per-lane) length
     Lvl src;            // compact source level (depth a > 0)
@@ -354,6 +355,34 @@ PCUB_HD T* launder(T* p) {
 #endif
     return p;
 }
+
+// a wave-uniform pointer kept in SGPRs (the same laundering for a base every lane shares)
+template <class T>
+PCUB_HD T* launder_s(T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(p));
+#endif
+    return p;
+}
+
+// a 64-bit value every lane of the wave holds, moved to SGPRs
+PCUB_HD long long uniform64(long long v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((unsigned long long)v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+#else
+    return v;
+#endif
+}
+
+// wave-uniform base + 32-bit lane byte offset: global loads with an SGPR base and a VGPR offset
+// (no 64-bit address arithmetic in the VALU)
+template <bool NT = false>
+PCUB_HD double2 ld2o(const double2* base, uint32_t lo) {
+    return ld2<NT>((const double2*)((const char*)base + lo));
+}
+PCUB_HD double ld1nto(const double* base, uint32_t lo) { return ld1nt((const double*)((const char*)base + lo)); }
 
 // Keeps the scheduler from hoisting the next column's loads above this point
 // (bounds the live registers of the unrolled final pass).

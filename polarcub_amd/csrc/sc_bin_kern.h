@@ -48,7 +48,8 @@ inline size_t bin_ylds_bytes(int v, int n) {
     return kVar[v].Y ? (size_t)kBinBlock * (((size_t)1 << n) / kVar[v].G / 32) * sizeof(uint32_t) : 0;
 }
 
-template <int S, int G, int W, bool LDS, int NT, bool YL = false, bool HL = false, int PF = 0, bool CR = false>
+template <int S, int G, int W, bool LDS, int NT, bool YL = false, bool HL = false, int PF = 0, bool CR = false,
+          bool TR = false>
 __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
     // [S pairs][kBinBlock] when LDS (HL: [S doubles][kBinBlock]), then [Nv/32 words][kBinBlock]
     // when YL (plus occupancy padding)
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_codeword<S, G, LDS, NT, YL, HL, PF, CR>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last,
+        decode_codeword<S, G, LDS, NT, YL, HL, PF, CR, -1, TR>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last,
                                                YL ? (uint32_t*)(lds_last + LDS2) + threadIdx.x : nullptr, kBinBlock,
                                                HL ? (double*)lds_last + threadIdx.x : nullptr);
     }
@@ -80,5 +81,8 @@ BinKernFn bin_kernel_part4(int v);
 BinKernFn bin_kernel_part5(int v);
 // the compact-root twin of variant v (CR: root rows as compact normalised doubles), or nullptr
 BinKernFn bin_kernel_compact(int v);
+// variant v reading its root in the wave's own tiles (TR: tile = 64 / G, a wave-uniform base and
+// 32-bit lane offsets), pairs or compact rows; nullptr where not instantiated (sc_bin_k7.hip)
+BinKernFn bin_kernel_tiled_root(int v, bool compact);
 
 }  // namespace pcub

@@ -46,16 +46,16 @@ PCUB_HD void col_load(const Chain& c, int p, int C, ColLoad<F, FG, R>& L) {
             // (a, b) of column P at x[2m], of column P+1 at x[2m+1]
             const long long q0 = root_row(P, c.nv);
             const long long q1 = q0 + (1LL << (c.nv - 2));
-            L.x[2 * m + 0] = double2{ld1nt(c.inc + (2 * q0) * c.B), ld1nt(c.inc + (2 * q0 + 1) * c.B)};
-            L.x[2 * m + 1] = double2{ld1nt(c.inc + (2 * q1) * c.B), ld1nt(c.inc + (2 * q1 + 1) * c.B)};
+            L.x[2 * m + 0] = double2{ld1nto(c.inc + (2 * q0) * c.B, c.lin), ld1nto(c.inc + (2 * q0 + 1) * c.B, c.lin)};
+            L.x[2 * m + 1] = double2{ld1nto(c.inc + (2 * q1) * c.B, c.lin), ld1nto(c.inc + (2 * q1 + 1) * c.B, c.lin)};
         } else if constexpr (R != 0) {
             // positions P, P + Nv/2 are rows (2q, 2q+1); P+1 adds Nv/4 to q
             const long long q0 = root_row(P, c.nv);
             const long long q1 = q0 + (1LL << (c.nv - 2));
-            L.x[4 * m + 0] = ld2<R == 2>(c.in + (2 * q0) * c.B);
-            L.x[4 * m + 1] = ld2<R == 2>(c.in + (2 * q0 + 1) * c.B);
-            L.x[4 * m + 2] = ld2<R == 2>(c.in + (2 * q1) * c.B);
-            L.x[4 * m + 3] = ld2<R == 2>(c.in + (2 * q1 + 1) * c.B);
+            L.x[4 * m + 0] = ld2o<R == 2>(c.in + (2 * q0) * c.B, c.lin);
+            L.x[4 * m + 1] = ld2o<R == 2>(c.in + (2 * q0 + 1) * c.B, c.lin);
+            L.x[4 * m + 2] = ld2o<R == 2>(c.in + (2 * q1) * c.B, c.lin);
+            L.x[4 * m + 3] = ld2o<R == 2>(c.in + (2 * q1 + 1) * c.B, c.lin);
         } else {
             L.x[2 * m + 0] = ld2<NS, GL>(c.src.p + (long long)(P >> 1) * c.src.s);
             L.x[2 * m + 1] = ld2<NS, GL>(c.src.p + (long long)((P + H * C) >> 1) * c.src.s);
@@ -294,7 +294,7 @@ PCUB_HD uint64_t hl_frozen(uint64_t* ub, const uint64_t* fv, int j) {
 //     hl, second half in registers; hl_run), one stored stage depth fewer than the plain S
 // PF: prefetch distance of the final passes (column pairs whose loads are in flight ahead)
 template <int S, int G, bool LDS = false, int NT = 0, bool YL = false, bool HL = false, int PF = 0, bool CR = false,
-          int PF1 = -1>
+          int PF1 = -1, bool TR = false>
 PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, long long slot, bool store,
                              Lvl last = Lvl{nullptr, 0}, uint32_t* ylds = nullptr, long long ystride = 0,
                              double* hl = nullptr) {
@@ -317,9 +317,21 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     const long long ns = A.nslots;
     const long long B = A.B;
     const long long rs = root_stride(A);  // root row stride: B ([N][B] rows) or the tile width
-    const long long rowbase = root_base(A, cw) + 2 * (long long)bitrev((uint32_t)j, n - 1) * rs;
-    const double2* in = CR ? nullptr : A.xy + rowbase;
-    const double* inc = CR ? A.xc + rowbase : nullptr;
+    // TR (tiled root, tile = the wave's 64 / G codewords): the wave's tile is one contiguous block,
+    // its base wave-uniform (SGPRs) and this lane's rows a 32-bit byte offset into it, so a root load
+    // is a global load with an SGPR base and a VGPR offset -- no 64-bit address add in the VALU.
+    // Otherwise a per-lane pointer (64-bit adds per load).
+    long long tbase, lrow;
+    if constexpr (TR) {
+        tbase = uniform64((cw / A.tile) * ((long long)A.tile << n));
+        lrow = cw % A.tile + 2 * (long long)bitrev((uint32_t)j, n - 1) * rs;
+    } else {
+        tbase = root_base(A, cw) + 2 * (long long)bitrev((uint32_t)j, n - 1) * rs;
+        lrow = 0;
+    }
+    const double2* in = CR ? nullptr : A.xy + tbase;
+    const double* inc = CR ? A.xc + tbase : nullptr;
+    const uint32_t lin = (uint32_t)(lrow * (CR ? 8 : 16));
     double2* scr = A.scratch + slot;
     uint32_t* Y = YL ? ylds : A.ybits + slot;
     const long long ys = YL ? ystride : ns;  // Y word stride
@@ -340,8 +352,13 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     int infow = 0;
 
     for (int k = 0; k < (1 << D); ++k) {
-        if constexpr (CR) inc = launder(inc);
-        else in = launder(in);
+        if constexpr (TR) {
+            if constexpr (CR) inc = launder_s(inc);
+            else in = launder_s(in);
+        } else {
+            if constexpr (CR) inc = launder(inc);
+            else in = launder(in);
+        }
         scr = launder(scr);
         if constexpr (!YL) Y = launder(Y);
         lm.scr = scr;
@@ -358,6 +375,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
         Chain c;
         c.in = in;
         c.inc = inc;
+        c.lin = lin;
         c.B = rs;
         c.nv = nv;
         c.Y = Y;

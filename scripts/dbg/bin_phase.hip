@@ -72,6 +72,7 @@ __device__ void decode_timed(const BinArgs& A, long long cw, int j, int lane, lo
         bool fg = (k != 0);
         Chain c;
         c.in = in;
+        c.lin = 0;
         c.inc = nullptr;
         c.B = root_stride(A);
         c.nv = nv;

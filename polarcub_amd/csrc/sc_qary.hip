@@ -73,6 +73,7 @@ int g_qylds = 1;   // symbols in LDS where a twin kernel exists and fits (pcub_s
 constexpr size_t kQLdsPerCu = 160 * 1024;
 int g_qregs = 0;   // cap on register positions per lane (pcub_sc_set_qary_regs; 0 = the default)
 int g_qhl = 1;     // split last level (HL twin) where one exists and fits (pcub_sc_set_qary_hl)
+int g_qtr = 1;     // the uniform-base twin for rows in the wave's own tiles (pcub_sc_set_qary_tiled_root)
 
 // register positions per lane S and lanes per codeword G for a code of 2^n:
 // S = 8 (q <= 4) or 4, G = the requested lanes, both reduced until N >= 2*S*G
@@ -205,7 +206,11 @@ int decode_qary_impl(const double* xy, int64_t B, int32_t log2N, int32_t q, int3
     char* slots = (char*)workspace + tb;
     A.scratch = (double2*)slots;
     A.ysym = c.yl ? nullptr : (uint32_t*)(slots + (size_t)A.nslots * (N / c.G - 2 * c.sr()) * ((q + 1) / 2) * sizeof(double2));
-    hipLaunchKernelGGL(qkernel(q, log2N), dim3((unsigned)g), dim3(kQBlock), qlaunch_lds(q, log2N), st, A);
+    // rows in the wave's own tiles: the uniform-base twin where one is instantiated
+    QKern kern = nullptr;
+    if (g_qtr && c.hl && tile == 64 / c.G) kern = qary_kernel_h_tr(q, c.S, c.G);
+    if (!kern) kern = qkernel(q, log2N);
+    hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(kQBlock), qlaunch_lds(q, log2N), st, A);
     return (int)hipGetLastError();
 }
 
@@ -270,6 +275,14 @@ extern "C" int pcub_sc_set_qary_hl(int on) {
 // Tuning hook (not part of the stable ABI): cap on the register positions per lane of
 // the q-ary decode kernel (0 = default: 8 for q <= 4, else 4; otherwise 2 or 4).
 // Returns the previous value.
+// Tuning hook (not part of the stable ABI): allow (1, the default) or forbid (0) the uniform-base
+// twin for rows in the wave's own tiles.  Returns the previous value.
+extern "C" int pcub_sc_set_qary_tiled_root(int on) {
+    const int old = g_qtr;
+    g_qtr = on ? 1 : 0;
+    return old;
+}
+
 extern "C" int pcub_sc_set_qary_regs(int S) {
     if (S != 0 && S != 2 && S != 4 && S != 8) return PCUB_EINVAL;
     const int old = g_qregs;

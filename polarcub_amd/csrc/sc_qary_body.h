@@ -319,6 +319,7 @@ PCUB_HD void q_store2(double2* base, long long pos, long long stride, const QV<Q
 // level a+e at positions c + m*C, m < 2^(F-e).
 struct QPass {
     const double* in;     // root: half-split position p of lane j is row rowbase + bitrev_{nv}(p)
+    uint32_t lin;         // TR: this lane's byte offset from in (a wave-uniform tile base); else 0
     long long B;
     int nv;               // log2 of the virtual (per-lane) length
     const double2* src;   // stored source level (a > 0)
@@ -331,7 +332,8 @@ struct QPass {
 
 template <int Q, bool ROOT>
 PCUB_HD QV<Q> q_src(const QPass& P, int pos) {
-    if constexpr (ROOT) return q_load<Q>(P.in, (long long)bitrev((uint32_t)pos, P.nv) * P.B * Q);
+    if constexpr (ROOT)
+        return q_load<Q>((const double*)((const char*)(P.in + (long long)bitrev((uint32_t)pos, P.nv) * P.B * Q) + P.lin), 0);
     else return q_load2<Q>(P.src, pos, P.ns);
 }
 
@@ -483,7 +485,7 @@ PCUB_HD void q_final_dispatch(const QPass& P, QV<Q>* v, bool gop, bool root, dou
 // HL: the chain ends at a split level of 2S positions per lane (the first S in the LDS column
 //     hl, the rest in registers; q_hl_run): one stored stage depth fewer (8qN bytes written and
 //     8qN read less per codeword)
-template <int Q, int S, int G = 1, int U = 1, bool YL = false, bool HL = false>
+template <int Q, int S, int G = 1, int U = 1, bool YL = false, bool HL = false, bool TR = false>
 PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store, int j = 0, int lane = 0,
                             uint32_t* ylds = nullptr, long long ystride = 0, double* hl = nullptr) {
     constexpr int SR = HL ? 2 * S : S;  // positions per lane at the chain's last level
@@ -504,10 +506,20 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
     // tiled layout: codeword cw's row 0 at ((cw / T) N) T + cw % T, rows T apart
     const long long rs = A.tile > 0 ? (long long)A.tile : A.B;
     const long long rb = A.tile > 0 ? (cw / A.tile) * ((long long)A.tile << A.n) + cw % A.tile : cw;
-    const double* in = A.xy + (rb + (long long)bitrev((uint32_t)j, A.n) * rs) * Q;
+    // TR (tile = the wave's 64 / G codewords): the tile's base wave-uniform (SGPRs), this lane's rows
+    // a 32-bit byte offset (binary decode_codeword's TR)
+    const double* in;
+    uint32_t lin = 0;
+    if constexpr (TR) {
+        in = A.xy + uniform64((cw / A.tile) * ((long long)A.tile << A.n)) * Q;
+        lin = (uint32_t)((cw % A.tile + (long long)bitrev((uint32_t)j, A.n) * rs) * Q * 8);
+    } else {
+        in = A.xy + (rb + (long long)bitrev((uint32_t)j, A.n) * rs) * Q;
+    }
     QInfo qi{A.info, A.B, cw, store, 0, j, G - 1, 0u};
     for (int k = 0; k < (1 << D); ++k) {
-        in = launder(in);
+        if constexpr (TR) in = launder_s(in);
+        else in = launder(in);
         scr = launder(scr);
         if constexpr (!YL) Y = launder(Y);
         const int d0 = (k == 0) ? 1 : D - __builtin_ctz((unsigned)k);
@@ -517,6 +529,7 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
         bool gop = (k != 0);
         QPass P;
         P.in = in;
+        P.lin = lin;
         P.B = rs;
         P.nv = nv;
         P.ns = ns;

@@ -32,4 +32,10 @@ QKern qary_kernel_q4_h(int S, int G) {
     return nullptr;
 }
 
+// ... reading its root rows in the wave's own tiles (TR: tile = 16, a wave-uniform base)
+QKern qary_kernel_q4_h_tr(int S, int G) {
+    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 3, 1, true, true, true>;
+    return nullptr;
+}
+
 }  // namespace pcub

@@ -1274,7 +1274,7 @@ def fx_harness_names(R, timing):
     """Which module attributes the reference harnesses bind (test.py, test2.py, test3.py,
     main_deletion.py, combine_codes.py; an AST scan), whether the reference module defines each
     one, and the observed behaviour of the entry points whose reference behaviour is a stub or a
-    failure (makeAWGN, encodeListDecodeSimulation, the q-ary genie, make_cmp_function) plus a few
+    failure (makeAWGN, encodeListDecodeSimulation, the q-ary genie) plus a few
     small helper values (the binary upgrade split, the q-ary cost bounds, makeQuantizedUniform)."""
     import importlib
     QMD, QPED, BMD = R["QMD"], R["QPED"], R["BMD"]
@@ -1304,8 +1304,6 @@ def fx_harness_names(R, timing):
         2, 8, make_x, lambda e: e, _qsc_channel_closure(qsc), make_xy, 3, {0, 1, 2, 4}, 2, 1))
     beh["qary_genieEncodeDecodeSimulation"] = _outcome(lambda: QPED.genieEncodeDecodeSimulation(
         8, make_x, lambda e: e, _qsc_channel_closure(qsc), make_xy, 2, 0.1, 7))
-    beh["make_cmp_function_odd"] = _outcome(lambda: QPED.make_cmp_function([0.1, 0.2, 0.3, 0.4])(1, 3))
-    beh["prefix_odd"] = _outcome(lambda: list(QPED.prefix(5)))
     beh["normalize"] = _outcome(lambda: [np.asarray(QPED.normalize(np.array([0.5, 2.0, 1.0]))[0]).tolist(),
                                          float(QPED.normalize(np.array([0.5, 2.0, 1.0]))[1])])
     beh["normalize_log"] = _outcome(lambda: [np.asarray(QPED.normalize(np.array([-3.0, -1.0]), True)[0]).tolist(),

@@ -418,32 +418,6 @@ def normalizeDistList(dist_list):
     return dist_list, normalization_vector
 
 
-def prefix(x):
-    """The reference's helper (:1208-1213): (x, 0) for odd x.  For even x its loop never ends
-    (`x >> 2` discards its result); here that case raises instead of hanging."""
-    if x % 2 == 0:
-        raise RuntimeError("prefix(): the reference loops forever on an even argument (QaryPolarEncoderDecoder.py:1210-1212)")
-    return x, 0
-
-
-def make_cmp_function(TVPlusPeVec):
-    """The reference's unused comparator factory (:1193-1206): its fall-through branch calls
-    math.sign, which does not exist, so every comparison of two odd indices prints "s" and
-    raises AttributeError, as there."""
-    def cmp_function(a, b):
-        a_prefix, a_suffix_len = prefix(a)
-        b_prefix, b_suffix_len = prefix(b)
-        if a_suffix_len > b_suffix_len and b >> (a_suffix_len - b_suffix_len) == a_prefix:
-            print("a")
-            return 1
-        if a_suffix_len < b_suffix_len and a >> (b_suffix_len - a_suffix_len) == b_prefix:
-            print("b")
-            return -1
-        print("s")
-        return math.sign(TVPlusPeVec[a], TVPlusPeVec[b])
-    return cmp_function
-
-
 def hamming(x, y):
     return sum(np.asarray(x) != np.asarray(y))
 

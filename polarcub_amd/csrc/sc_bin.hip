@@ -18,14 +18,35 @@
 
 using namespace pcub;
 
+// A/B experiments (sc_bin_kx*.hip): kernels in their own namespaces, launched instead of the
+// tiled-root twin while pcub_sc_set_experiment(e) selects one.  Diagnostic hook, not the ABI.
+namespace pcubx1 { BinKernFn bin_kernel_x(int v, bool compact); }
+namespace pcubx2 { BinKernFn bin_kernel_x(int v, bool compact); }
+static BinKernFn exp_kernel(int e, int v, bool compact) {
+    switch (e) {
+        case 1: return pcubx1::bin_kernel_x(v, compact);
+        case 2: return pcubx2::bin_kernel_x(v, compact);
+        default: return nullptr;
+    }
+}
+static int g_experiment = 0;
+extern "C" int pcub_sc_set_experiment(int e) {
+    const int old = g_experiment;
+    g_experiment = e;
+    return old;
+}
+
 namespace {
 
 constexpr int kBlock = kBinBlock;
 
-// rate-0 table: one byte per register subtree (first_frozen_depth)
-__global__ __launch_bounds__(kBlock) void k_ef_table(const uint32_t* fmask, int D, int SU, uint8_t* ef) {
+// rate-0 table: one byte per register subtree (first_frozen_depth); information-bit compress masks:
+// eight words per frozen-mask word (compress_masks)
+__global__ __launch_bounds__(kBlock) void k_ef_table(const uint32_t* fmask, int D, int SU, uint8_t* ef, int nwords,
+                                                     uint32_t* cmask) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     if (k < (1 << D)) ef[k] = (uint8_t)first_frozen_depth(fmask, k, D, SU);
+    if (k < nwords) compress_masks(fmask[k], cmask + 8 * k);
 }
 
 template <int NN>
@@ -98,7 +119,9 @@ int tree_depth(int n, int v) {
     while ((1 << s) < bin_sr(v)) ++s;
     return n - g - s;
 }
-size_t ef_bytes(int n, int v) { return (((size_t)1 << tree_depth(n, v)) + 255) & ~(size_t)255; }
+size_t ef_only_bytes(int n, int v) { return (((size_t)1 << tree_depth(n, v)) + 255) & ~(size_t)255; }
+size_t cmask_words(int n) { return n >= 5 ? ((size_t)1 << n) / 32 : 1; }
+size_t ef_bytes(int n, int v) { return ef_only_bytes(n, v) + ((cmask_words(n) * 32 + 255) & ~(size_t)255); }
 
 // per-slot bytes: virtual levels 1..D-1 (Nv/2 - S pairs) + Nv local encoding bits (unless in LDS)
 size_t slot_bytes(int n, int v) {
@@ -212,6 +235,7 @@ int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N
     A.ybits = nullptr;
     A.nslots = 0;
     A.ef = nullptr;
+    A.cmask = nullptr;
     A.tile = tile;
     if (log2N <= 5) {
         const dim3 grid((unsigned)((B + kBlock - 1) / kBlock));
@@ -237,16 +261,21 @@ int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N
     const size_t Nv = ((size_t)1 << log2N) / kVar[v].G;
     const int D = tree_depth(log2N, v);
     uint8_t* ef = (uint8_t*)workspace;
+    uint32_t* cmask = (uint32_t*)((char*)workspace + ef_only_bytes(log2N, v));
     char* slots = (char*)workspace + efb;
-    hipLaunchKernelGGL(k_ef_table, dim3((unsigned)(((1 << D) + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, frozen_mask,
-                       D, bin_sr(v) * kVar[v].G, ef);
+    const int nw = (int)cmask_words(log2N);
+    const int eft = (1 << D) > nw ? (1 << D) : nw;
+    hipLaunchKernelGGL(k_ef_table, dim3((unsigned)((eft + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, frozen_mask,
+                       D, bin_sr(v) * kVar[v].G, ef, nw, cmask);
     A.ef = ef;
+    A.cmask = cmask;
     A.nslots = nslots;
     A.scratch = (double2*)slots;
     A.ybits = kVar[v].Y ? nullptr : (uint32_t*)(slots + (size_t)nslots * (Nv / 2 - bin_sr(v)) * sizeof(double2));
     // rows in the wave's own tiles: the uniform-base twin where one is instantiated
     BinKernFn kern = nullptr;
-    if (g_tiled_root && tile == 64 / kVar[v].G) kern = bin_kernel_tiled_root(v, xc != nullptr);
+    if (g_experiment && tile == 64 / kVar[v].G) kern = exp_kernel(g_experiment, v, xc != nullptr);
+    if (!kern && g_tiled_root && tile == 64 / kVar[v].G) kern = bin_kernel_tiled_root(v, xc != nullptr);
     if (!kern) kern = xc ? bin_kernel_compact(v) : variant_kernel(v);
     if (!kern) return PCUB_EINVAL;
     hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(kBlock), launch_lds(v, log2N), st, A);

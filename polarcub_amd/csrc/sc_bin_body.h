@@ -47,7 +47,43 @@ struct BinArgs {
     long long nslots;
     const uint8_t* ef;         // [2^D] first rate-0 depth of each subtree's chain (first_frozen_depth)
     int tile;                  // root layout: 0 = [N][B] rows; T > 0 = [ceil(B/T)][N][T] (T codewords a tile)
+    const uint32_t* cmask;     // [N/32][8] per frozen-mask word: compress masks mv0..mv4, info count, info mask
 };
+
+// Information-bit compress masks of one 32-bit frozen-mask word (Hacker's Delight 7-4, "compress"):
+// with m = ~fm the information positions, x -> the bits of x at m packed to the right is
+//     x &= m;  for i in 0..4: t = x & mv_i;  x = (x ^ t) | (t >> 2^i)
+// and mv_i depends on m alone, so the decode kernel gets them from a table built once per launch.
+// out[0..4] = mv_i, out[5] = popcount(m), out[6] = m, out[7] = 0.
+PCUB_HD void compress_masks(uint32_t fm, uint32_t* out) {
+    uint32_t m = ~fm;
+    out[5] = (uint32_t)__builtin_popcount(m);
+    out[6] = m;
+    out[7] = 0u;
+    uint32_t mk = ~m << 1;
+    for (int i = 0; i < 5; ++i) {
+        uint32_t mp = mk ^ (mk << 1);
+        mp ^= mp << 2;
+        mp ^= mp << 4;
+        mp ^= mp << 8;
+        mp ^= mp << 16;
+        const uint32_t mv = mp & m;
+        out[i] = mv;
+        m = (m ^ mv) | (mv >> (1 << i));
+        mk &= ~mp;
+    }
+}
+
+// the bits of x at the information positions of word `cm` (compress_masks), packed to the right
+PCUB_HD uint32_t compress_info(uint32_t x, const uint32_t* cm) {
+    x &= cm[6];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t t = x & cm[i];
+        x = (x ^ t) | (t >> (1 << i));
+    }
+    return x;
+}
 
 // Offset (in rows' elements) of codeword cw's root row 0, and the stride between root rows.
 PCUB_HD long long root_base(const BinArgs& A, long long cw) {

@@ -283,6 +283,86 @@ PCUB_HD uint64_t hl_frozen(uint64_t* ub, const uint64_t* fv, int j) {
     return ((uint64_t)((ym ^ yp) & SM)) | ((uint64_t)(yp & SM) << S);
 }
 
+#ifndef PCUB_R5
+#define PCUB_R5 0
+#endif
+
+// byte permute (v_perm_b32): result byte i = byte sel_i of the 8-byte value {hi, lo} (0..3: lo)
+PCUB_HD uint32_t perm_bytes(uint32_t hi, uint32_t lo, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) r |= (uint32_t)((v >> (8 * ((sel >> (8 * i)) & 7))) & 0xffu) << (8 * i);
+    return r;
+#endif
+}
+
+// 4x4 byte transpose: out[b] byte k = in[k] byte b (v_perm_b32, eight of them)
+PCUB_HD void bytes_t4(const uint32_t* in, uint32_t* out) {
+    const uint32_t a0 = perm_bytes(in[1], in[0], 0x05010400u);  // in0.0 in1.0 in0.1 in1.1
+    const uint32_t a1 = perm_bytes(in[1], in[0], 0x07030602u);  // in0.2 in1.2 in0.3 in1.3
+    const uint32_t a2 = perm_bytes(in[3], in[2], 0x05010400u);
+    const uint32_t a3 = perm_bytes(in[3], in[2], 0x07030602u);
+    out[0] = perm_bytes(a2, a0, 0x05040100u);
+    out[1] = perm_bytes(a2, a0, 0x07060302u);
+    out[2] = perm_bytes(a3, a1, 0x05040100u);
+    out[3] = perm_bytes(a3, a1, 0x07060302u);
+}
+
+// x_hat from a lane's local re-encoded bits: x_hat local word w, bit t is Y bit bitrev_nv(32w + t)
+// = Y bit (bitrev5(t) 2^R + bitrev_R(w)), R = nv - 5.  With Z'[t][c] = Y bit (bitrev5(t) 2^R + c)
+// (Z = Y as 32 rows of 2^R bits, rows taken in bit-reversed order), word w is column bitrev_R(w)
+// of Z' (bit t = Z'[t][c]): a bit-matrix transpose instead of 32 single-bit gathers per word.
+// R = 3 (nv = 8): Z's rows are the 32 bytes of Y.  Z' rows 8k .. 8k+7 are byte bitrev2(k) of the Y
+// words bitrev3(0..7) = 0,4,2,6,1,5,3,7 (byte transposes of those word groups), an 8x8 bit transpose
+// per block makes byte c of block k column c's bits 8k .. 8k+7, and byte transposes gather them.
+PCUB_HD void xhat_r3(const uint32_t* y, uint32_t* out) {
+    const uint32_t ga[4] = {y[0], y[4], y[2], y[6]}, gb[4] = {y[1], y[5], y[3], y[7]};
+    uint32_t la[4], lb[4];
+    bytes_t4(ga, la);
+    bytes_t4(gb, lb);
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int b = (int)bitrev((uint32_t)k, 2);
+        uint64_t x = (uint64_t)la[b] | ((uint64_t)lb[b] << 32);  // byte i = row 8k + i of Z'
+        uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+        x ^= t ^ (t << 7);
+        t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+        x ^= t ^ (t << 14);
+        t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+        x ^= t ^ (t << 28);  // byte c = column c over rows 8k .. 8k+7
+        lo[k] = (uint32_t)x;
+        hi[k] = (uint32_t)(x >> 32);
+    }
+    uint32_t col[8];
+    bytes_t4(lo, col);
+    bytes_t4(hi, col + 4);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) out[w] = col[(int)bitrev((uint32_t)w, 3)];
+}
+
+// R = 5 (nv = 10): Z' rows are the Y words in bit-reversed order (a[r] = Y word bitrev5(r)); a
+// 32x32 bit transpose in place.
+PCUB_HD void xhat_r5(uint32_t* a, uint32_t* out) {
+    constexpr uint32_t M[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const int jj = 16 >> s;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            if (k & jj) continue;
+            const uint32_t t = ((a[k] >> jj) ^ a[k + jj]) & M[s];
+            a[k + jj] ^= t;
+            a[k] ^= t << jj;
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < 32; ++w) out[w] = a[(int)bitrev((uint32_t)w, 5)];
+}
+
 // Decode codeword `cw` (clamped to a valid index for loads) with lane j of its
 // G lanes (`lane` = wave lane id, for the exchanges) in scratch slot `slot`.
 // S = virtual register subtree (values per lane) in {8, 16, 32}; requires
@@ -350,6 +430,9 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     uint64_t acc = 0;
     int nacc = 0;
     int infow = 0;
+#if PCUB_R5
+    uint32_t acc32 = 0;
+#endif
 
     for (int k = 0; k < (1 << D); ++k) {
         if constexpr (TR) {
@@ -481,6 +564,30 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
             }
         }
         // information bits of this subtree, in u order (identical in all G lanes)
+#if PCUB_R5
+        if constexpr (W::SUW >= 32) {
+            // per 32-bit word of the window: the information bits packed by the precomputed compress
+            // masks (all-frozen words skipped, all-information words taken whole), then appended
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+#pragma unroll
+                for (int h = 0; h < W::SUW / 32; ++h) {
+                    const uint32_t* cm = A.cmask + (long long)((k * SU + 64 * w) / 32 + h) * 8;
+                    const int cnt = (int)cm[5];
+                    if (cnt == 0) continue;
+                    uint32_t x = (uint32_t)(ub[w] >> (32 * h));
+                    if (cnt != 32) x = compress_info(x, cm);
+                    acc32 |= x << nacc;
+                    if (nacc + cnt >= 32) {
+                        if (store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = acc32;
+                        acc32 = nacc ? (x >> (32 - nacc)) : 0u;
+                        ++infow;
+                    }
+                    nacc = (nacc + cnt) & 31;
+                }
+            }
+        } else
+#endif
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             for (uint64_t im = ~fm[w] & W::WMASK; im != 0ull; im &= im - 1ull) {
@@ -512,8 +619,31 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
                 sty<YL>(base + (long long)w * ys, ldy<YL>(base + (long long)w * ys) ^ ldy<YL>(base + (long long)(w + Wc) * ys));
         }
     }
+#if PCUB_R5
+    if constexpr (W::SUW >= 32) acc = acc32;
+#endif
     if (nacc && store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
     // x_hat natural segment k = bitrev_g(j) is this lane's local Y, bit-reversed over nv bits
+#if PCUB_R5
+    if (A.xhat && store && (nv == 8 || nv == 10)) {
+        const int seg = (int)bitrev((uint32_t)j, g);
+        if (nv == 8) {
+            uint32_t yw[8], o[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) yw[w] = ldy<YL>(Y + (long long)w * ys);
+            xhat_r3(yw, o);
+#pragma unroll
+            for (int w = 0; w < 8; ++w) A.xhat[(long long)(seg * 8 + w) * B + cw] = o[w];
+        } else {
+            uint32_t yw[32], o[32];
+#pragma unroll
+            for (int r = 0; r < 32; ++r) yw[r] = ldy<YL>(Y + (long long)bitrev((uint32_t)r, 5) * ys);
+            xhat_r5(yw, o);
+#pragma unroll
+            for (int w = 0; w < 32; ++w) A.xhat[(long long)(seg * 32 + w) * B + cw] = o[w];
+        }
+    } else
+#endif
     if (A.xhat && store) {
         const int seg = (int)bitrev((uint32_t)j, g);
         const int W = Nv >> 5;

@@ -56,6 +56,34 @@ PCUB_HD double cv_pack(double q, uint32_t s) {
     return from_bits(as_bits(q) | (long long)((unsigned long long)s << 63));
 }
 
+#ifndef PCUB_FAST_F
+#define PCUB_FAST_F 0
+#endif
+
+// RN(num / den) for the minus transform's normalisation: den = max(1 + ra*rb, ra + rb) in [1, 2]
+// (or NaN), num = the min in [0, 2].  The compiler's IEEE sequence without v_div_scale /
+// v_div_fixup: those only act near the ends of the exponent range (div_scale: a denominator or
+// quotient near overflow/underflow, a numerator below 2^-969; fixup: zero, inf, NaN operands).
+// Here den is in [1, 2]; a numerator below 2^-969 needs ra + rb < 2^-969, so ra*rb underflows and
+// den = 1 + 0 = 1 exactly, where y = rcp(1) = 1, q = num, r = 0: the exact quotient, which is what
+// the scaled sequence returns; num = 0 gives +0; NaN stays NaN.  Elsewhere the two sequences are
+// the same operations on the same values (rcp, two Newton steps, q = num*y, r = fma(-den, q, num),
+// fma(r, y, q)), bit for bit.
+PCUB_HD double div_den12(double num, double den) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double y = __builtin_amdgcn_rcp(den);
+    double e = __builtin_fma(-den, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-den, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    const double q = num * y;
+    const double r = __builtin_fma(-den, q, num);
+    return __builtin_fma(r, y, q);
+#else
+    return num / den;
+#endif
+}
+
 // max-normalise an un-normalised pair (p0, p1 >= 0) into compact form;
 // (0, 0) gives 0/0 = NaN, the sentinel.
 PCUB_HD double norm_pack(double p0, double p1) {
@@ -79,7 +107,11 @@ PCUB_HD double op_f(double va, double vb) {
     // does; on a tie both are the same value.
     const double num = __builtin_fmin(p0, p1);
     const double den = __builtin_fmax(p0, p1);  // in [1, 2], or NaN
+#if PCUB_FAST_F
+    return cv_pack(div_den12(num, den), a.s ^ b.s ^ (sw ? 1u : 0u));
+#else
     return cv_pack(num / den, a.s ^ b.s ^ (sw ? 1u : 0u));
+#endif
 }
 
 // plus transform (BinaryMemorylessVectorDistribution.py:31-47) + normalise.
@@ -98,7 +130,13 @@ PCUB_HD double op_g(double va, double vb, uint32_t u) {
         const bool agt = a.r > b.r;
         const double mx = agt ? a.r : b.r;
         const double mn = agt ? b.r : a.r;
+#if PCUB_FAST_F
+        // one comparison: where neither is greater the quotient is 1 (the tie (1, 1), either sign)
+        // or NaN (the (0, 0) sentinel, either sign), so b.s ^ !agt is as good as b.r > a.r there
+        s = b.s ^ (agt ? 0u : 1u);
+#else
         s = b.s ? (agt ? 1u : 0u) : (b.r > a.r ? 1u : 0u);
+#endif
         q = mn / mx;
     }
     return cv_pack(q, s);

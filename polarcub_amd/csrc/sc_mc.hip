@@ -165,20 +165,26 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel(McArgs A, const uint32_
 // ratio p0 / p1 = exp(2y / sigma^2), so the row is (1, exp(-2y/s2)) for y >= 0, else
 // (exp(2y/s2), 1); BSC: makeBSC's row normalised (norm_pack).
 //
-// Draws (round 4): elements 4j..4j+3 of codeword g take the four words of Philox counter
-// (g, kStreamChannel, j) as 32-bit uniforms u = (r + 1) 2^-32 in (0, 1]: BI-AWGN pairs them into
-// two f32 Box-Muller transforms (|z| <= 6.66 at u = 2^-32) and forms y, 2y/s2 and exp(-|2y/s2|)
-// in f32, stored as the f64 row value; BSC flips where u <= p.  The noise is a simulation draw,
-// not a reference value: f32 rounds each row to a relative 6e-8, far below anything a frame-error
-// rate resolves, and the decode's arithmetic on the stored rows is the reference's in f64
-// (test_gpu_fer.py holds the FER to the reference's own runs).
+// Draws (round 5).  BSC: elements 4j..4j+3 of codeword g take the four words of Philox counter
+// (g, kStreamChannel, j) as 32-bit uniforms u = (r + 1) 2^-32 in (0, 1] and flip where u <= p.
+// BI-AWGN: elements 4j..4j+3 take counters (g, kStreamChannel, 2j) and (g, kStreamChannel, 2j+1):
+// the first gives two 53-bit uniforms (the Box-Muller radii, so the tail reaches |z| = 8.6 as with
+// f64 draws; a 32-bit radius stops at 6.66, below which sigma ~ 0.15 could never flip a bit), the
+// second two 32-bit uniforms for the angles.  The transforms run in f32 (v_log_f32, v_sqrt_f32, sin /
+// cos by pi-scaled reduction), and so do y, l = 2y/s2 and exp(-|l|) while |l| < 80; past that the
+// f32 exp would underflow (to 0 at |l| > ~103: a hard row the f64 reference never produces) and the
+// row is exp(-|l|) in f64.  The noise is a simulation draw, not a reference value: f32 rounds a row
+// to a relative 6e-8, far below anything a frame-error rate resolves, and the decode's arithmetic on
+// the stored rows is the reference's in f64 (test_gpu_fer.py holds the FER to the reference's runs,
+// test_gpu_mc.py the rows at 20 dB).
 __device__ __forceinline__ float u01f(uint32_t r) { return ((float)r + 1.0f) * 2.3283064365386963e-10f; }
 
 __device__ __forceinline__ double awgn_normf(const McArgs& A, uint32_t xb, float z) {
     const float y = (xb ? -1.0f : 1.0f) + (float)A.sigma * z;
     const float l = y * (float)(A.inv2s2 * 4.0);  // 2 y / sigma^2
-    const float r = expf(-__builtin_fabsf(l));
-    return l >= 0.0f ? (double)r : -(double)r;
+    const float al = __builtin_fabsf(l);
+    const double r = al < 80.0f ? (double)expf(-al) : exp(-(double)al);
+    return l >= 0.0f ? r : -r;
 }
 
 __device__ __forceinline__ void put_norm(double* out, long long at, double c, bool compact) {
@@ -202,19 +208,23 @@ __global__ __launch_bounds__(kMcBlock) void k_mc_channel_norm(McArgs A, const ui
     for (long long j = blockIdx.y; j < quads; j += gridDim.y) {
         const long long i0 = 4 * j;
         const uint32_t xw = x[(i0 >> 5) * A.B + b] >> (i0 & 31);  // bits i0..i0+3 (one word: i0 % 4 == 0)
-        const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)j, (uint32_t)A.seed,
-                            (uint32_t)(A.seed >> 32));
         double c[4];
         if (A.channel == 0) {
+            const P4 ra = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)(2 * j),
+                                 (uint32_t)A.seed, (uint32_t)(A.seed >> 32));
+            const P4 rb = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)(2 * j + 1),
+                                 (uint32_t)A.seed, (uint32_t)(A.seed >> 32));
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const float rad = sqrtf(-2.0f * logf(u01f(r.v[2 * h])));
+                const float rad = sqrtf(-2.0f * logf((float)u01(ra.v[2 * h], ra.v[2 * h + 1])));
                 float sn, cs;
-                sincospif(2.0f * u01f(r.v[2 * h + 1]), &sn, &cs);
+                sincospif(2.0f * u01f(rb.v[h]), &sn, &cs);
                 c[2 * h] = awgn_normf(A, (xw >> (2 * h)) & 1u, rad * cs);
                 c[2 * h + 1] = awgn_normf(A, (xw >> (2 * h + 1)) & 1u, rad * sn);
             }
         } else {
+            const P4 r = philox((uint32_t)g, (uint32_t)(g >> 32), kStreamChannel, (uint32_t)j, (uint32_t)A.seed,
+                                (uint32_t)(A.seed >> 32));
             const double hi = 0.5 * (1.0 - A.param), lo = 0.5 * A.param;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {

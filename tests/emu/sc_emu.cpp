@@ -23,6 +23,7 @@ extern "C" int emu_decode_bin(const double* xy, long long B, int n, const uint32
     A.xhat = xhat;
     A.uout = uout;
     A.ef = nullptr;
+    A.cmask = nullptr;
     A.tile = 0;
     if (n <= 5) {
         for (long long b = 0; b < B; ++b) {
@@ -45,6 +46,9 @@ extern "C" int emu_decode_bin(const double* xy, long long B, int n, const uint32
     std::vector<uint8_t> ef((size_t)1 << D);
     for (int k = 0; k < (1 << D); ++k) ef[k] = (uint8_t)first_frozen_depth(fmask, k, D, S);
     A.ef = ef.data();
+    std::vector<uint32_t> cm((size_t)(N / 32) * 8);
+    for (int i = 0; i < N / 32; ++i) compress_masks(fmask[i], cm.data() + 8 * i);
+    A.cmask = cm.data();
     A.scratch = scr.data();
     A.ybits = yb.data();
     A.nslots = nslots;
@@ -82,6 +86,9 @@ extern "C" int emu_decode_bin_compact(const double* xc, long long B, int n, cons
     std::vector<uint8_t> ef((size_t)1 << D);
     for (int k = 0; k < (1 << D); ++k) ef[k] = (uint8_t)first_frozen_depth(fmask, k, D, SR);
     A.ef = ef.data();
+    std::vector<uint32_t> cm((size_t)(N / 32) * 8);
+    for (int i = 0; i < N / 32; ++i) compress_masks(fmask[i], cm.data() + 8 * i);
+    A.cmask = cm.data();
     A.scratch = scr.data();
     A.ybits = yb.data();
     A.nslots = nslots;

@@ -67,19 +67,6 @@ def test_encodeListDecodeSimulation_reference_failure_is_recorded():
     assert B["encodeListDecodeSimulation"]["error"] == "TypeError"
 
 
-def test_cmp_function_and_prefix():
-    ref = B["make_cmp_function_odd"]
-    import contextlib
-    import io
-    buf = io.StringIO()
-    with contextlib.redirect_stdout(buf), pytest.raises(AttributeError) as e:
-        coding_qary.make_cmp_function([0.1, 0.2, 0.3, 0.4])(1, 3)
-    assert str(e.value) == ref["message"] and buf.getvalue() == ref["stdout"]
-    assert list(coding_qary.prefix(5)) == B["prefix_odd"]["value"]
-    with pytest.raises(RuntimeError):
-        coding_qary.prefix(4)  # the reference never returns
-
-
 def test_normalize_helpers():
     v, m = coding_qary.normalize(np.array([0.5, 2.0, 1.0]))
     assert [v.tolist(), m] == B["normalize"]["value"]

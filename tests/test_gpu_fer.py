@@ -6,6 +6,8 @@ decoder, run in the build container by oracle/make_fer.py (tests/golden/fer_ref.
 test is a two-sample binomial test: |p_dev - p_ref| <= 4 sqrt(s_dev^2 + s_ref^2).
 
   C2  N=1024 K=512 BI-AWGN 2 dB (BinaryPolarEncoderDecoder.py:328-387's trial loop)
+  C3  N=4096 K=2048 BI-AWGN 2 dB (configs[2]'s code: the same trial loop at n=12), through the
+      chunked device pipeline mc.run_bin that bench.py's C3 line shards over ranks
   C4  q=4 N=256 K=128 QSC(0.11), the reference's degrading construction (QaryPolarEncoderDecoder.py:935-982)
   C5  deletion n=8 n0=2 pd=0.1 xi=0.1, main_deletion's construction (K=3) and the genie ranking at K=64
       (main_deletion.py:142-146)
@@ -38,7 +40,7 @@ def test_fixture_is_complete():
     """CPU: the fixture holds every configuration with enough trials for a useful interval."""
     with open(FIX) as f:
         d = json.load(f)
-    for name, need in (("C2", 20000), ("C4", 20000), ("C5", 50000), ("C5k64", 20000)):
+    for name, need in (("C2", 20000), ("C3", 20000), ("C4", 20000), ("C5", 50000), ("C5k64", 20000)):
         r = d[name]
         assert r["trials"] >= need and 0 <= r["frame_errors"] <= r["trials"]
         assert r["bit_errors"] >= r["frame_errors"]
@@ -57,6 +59,20 @@ def test_c2_awgn_fer_matches_reference():
     code = sc.CodeSpec.from_frozen_set(1 << n, set(np.nonzero(fr)[0].tolist()), 1, device="cuda")
     n_cw, fe, be, _ = mc.run_bin(code, 20250204, 0, 1 << 20, mc.CHANNEL_AWGN, s2)
     ok, info = _close(fe, n_cw, _ref("C2"))
+    assert ok, info
+
+
+@pytest.mark.gpu
+def test_c3_awgn_fer_matches_reference():
+    """configs[2]'s code at N=4096: 2^20 codewords through mc.run_bin in 2^18-codeword chunks (the
+    f32-channel pipeline, compact tiled rows into the N=4096 decode) against 24,000 reference trials."""
+    from polarcub_amd import construction, mc, sc
+    n, K = 12, 2048
+    s2 = construction.awgn_sigma2(2.0, K / (1 << n))
+    fr = construction.bhattacharyya_frozen(n, K, s2)
+    code = sc.CodeSpec.from_frozen_set(1 << n, set(np.nonzero(fr)[0].tolist()), 1, device="cuda")
+    n_cw, fe, be, _ = mc.run_bin(code, 20250205, 0, 1 << 20, mc.CHANNEL_AWGN, s2, chunk=1 << 18)
+    ok, info = _close(fe, n_cw, _ref("C3"))
     assert ok, info
 
 

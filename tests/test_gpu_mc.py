@@ -50,11 +50,69 @@ def test_sharded_counters_match_single_run(code, world):
     assert one[0] == total and 0 < one[1] < total
 
 
+def test_sharded_counters_match_single_run_n4096():
+    """C3's decomposition at its own code length (N=4096, K=2048): 8 ranks' shards of [0, total),
+    each run in chunks that do not divide it, sum to one run over [0, total) in other chunks."""
+    from polarcub_amd import construction, mc, sc
+    n, K = 12, 2048
+    s2 = construction.awgn_sigma2(2.0, K / (1 << n))
+    fr = construction.bhattacharyya_frozen(n, K, s2)
+    c = sc.CodeSpec.from_frozen_set(1 << n, set(np.nonzero(fr)[0].tolist()), 1, device="cuda")
+    total = 8 * 6000 + 5
+    one = mc.run_bin(c, 11, 0, total, mc.CHANNEL_AWGN, s2, chunk=16384)
+    parts = []
+    for r in range(8):
+        lo, hi = mc.shard_range(total, r, 8)
+        parts.append(mc.run_bin(c, 11, lo, hi - lo, mc.CHANNEL_AWGN, s2, chunk=2500))
+    summed = [sum(p[i] for p in parts) for i in range(4)]
+    assert summed == one
+    assert one[0] == total and 0 < one[1] < total
+
+
 def test_clean_channels_decode_error_free(code):
     from polarcub_amd import mc
     c, _ = code
     assert mc.run_bin(c, 3, 0, 20000, mc.CHANNEL_BSC, 0.0)[1:3] == [0, 0]
     assert mc.run_bin(c, 3, 0, 20000, mc.CHANNEL_AWGN, 0.05)[1:3] == [0, 0]
+
+
+def test_norm_rows_high_snr_stay_soft(code):
+    """at 20 dB (sigma^2 = 0.01, |2y/s2| around 200) the f32 exp would underflow to exact
+    zeros -- hard rows the f64 reference never produces.  Every compact row must be finite and
+    non-zero, its log-ratio -ln|r| = |2y/s2| (y = +-1 + sigma z), and its orientation = the sign of y."""
+    from polarcub_amd import mc
+    c, _ = code
+    s2 = 0.01
+    info, rows = mc.philox_norm_batch(c, 5, 0, 4096, mc.CHANNEL_AWGN, s2)
+    r = rows.abs()
+    assert bool(torch.isfinite(rows).all()) and bool((r > 0).all())
+    l = -torch.log(r)  # |2y / s2|
+    y = l * s2 / 2.0
+    assert abs(float(y.mean()) - 1.0) < 0.01  # |y| ~ 1 + sigma z, z ~ N(0, 1): mean 1, sd 0.1
+    assert abs(float(y.std()) - 0.1) < 0.01
+    assert float(l.max()) > 103.0  # past the f32 exp's underflow point, still soft
+
+
+def test_norm_rows_channel_law(code):
+    """The normalised AWGN rows (53-bit Box-Muller radii) against the pair generator's law: the
+    fraction of rows whose orientation disagrees with the sent bit is Q(1/sigma), and z = (|y| - 1) /
+    sigma has unit variance with the Gaussian's fourth moment (3)."""
+    from polarcub_amd import mc, sc
+    c, _ = code
+    s2 = 0.5
+    B = 1 << 14
+    info, rows = mc.philox_norm_batch(c, 9, 0, B, mc.CHANNEL_AWGN, s2)
+    x = sc.encode_native(c, info).cpu().numpy().view(np.uint32)
+    bits = ((x[:, None, :] >> np.arange(32, dtype=np.uint32)[None, :, None]) & 1).reshape(-1, B)[:c.N]
+    v = rows.cpu().numpy()
+    y = -np.log(np.abs(v)) * s2 / 2.0 * np.where(np.signbit(v), -1.0, 1.0)  # 2y/s2 = -ln r, signed
+    flips = float(np.mean((y < 0) != (bits == 1)))
+    q = 0.5 * math.erfc(1.0 / math.sqrt(2.0 * s2))
+    n = y.size
+    assert abs(flips - q) < 5 * math.sqrt(q * (1 - q) / n)
+    z = (y * np.where(bits == 1, -1.0, 1.0) - 1.0) / math.sqrt(s2)
+    assert abs(float(z.mean())) < 0.01 and abs(float(z.var()) - 1.0) < 0.01
+    assert abs(float(np.mean(z ** 4)) - 3.0) < 0.05
 
 
 def test_bsc_fer_agrees_with_reference_run():

@@ -46,7 +46,9 @@ extern "C" {
 
 #define PCUB_EINVAL (-1)
 
-/* Library version, for the loader's ABI check. */
+/* Library version, for the loader's ABI check.  3: the deletion state tables carry an 8-double
+ * header (size them with pcub_sc_deletion_table_bytes, never from the version-2 formula), and
+ * pcub_tile_pairs. */
 int pcub_abi_version(void);
 
 /* Bytes of device workspace pcub_sc_decode_bin needs for a batch of B
@@ -336,6 +338,12 @@ int pcub_unpack_bits(const uint32_t* words, int64_t B, int32_t nbits, uint8_t* b
 
 /* [B][N][q] f64 -> [N][B][q] f64, 1 <= q <= 8 (q = 2 for binary pairs). */
 int pcub_transpose_pairs(const double* src, int64_t B, int32_t N, int32_t q, double* dst, void* stream);
+
+/* [B][N][q] f64 -> the tiled layout [ceil(B/T)][N][T][q] f64 that pcub_sc_decode_bin_tiled /
+ * pcub_sc_decode_qary_tiled read (codeword b's row i at ((b / T) N + i) T + b % T; the last tile's
+ * padding columns zero), 1 <= q <= 8, 1 <= T <= 4096: the reference's per-codeword rows
+ * (BinaryMemorylessVectorDistribution.probs) in one pass into the layout the headline kernel reads. */
+int pcub_tile_pairs(const double* src, int64_t B, int32_t N, int32_t q, int32_t T, double* dst, void* stream);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,7 @@ _i32 = ctypes.c_int32
 _lib = None
 
 EINVAL = -1
-ABI_VERSION = 2  # include/polarcub_sc.h (2: guard-band ones in the deletion entry points)
+ABI_VERSION = 3  # include/polarcub_sc.h (2: guard-band ones in the deletion entry points; 3: table headers, tile_pairs)
 
 
 class HipError(RuntimeError):
@@ -74,6 +74,8 @@ def lib():
     L.pcub_unpack_bits.argtypes = [_c_void_p, _i64, _i32, _c_void_p, _c_void_p]
     L.pcub_transpose_pairs.restype = ctypes.c_int
     L.pcub_transpose_pairs.argtypes = [_c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p]
+    L.pcub_tile_pairs.restype = ctypes.c_int
+    L.pcub_tile_pairs.argtypes = [_c_void_p, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p]
     L.pcub_sc_deletion_supported.restype = ctypes.c_int
     L.pcub_sc_deletion_supported.argtypes = [_i32, _i32, _i32]
     L.pcub_sc_leaf_deletion_supported.restype = ctypes.c_int
@@ -191,7 +193,7 @@ def lib():
 # every exported symbol declared in include/polarcub_sc.h
 EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_bin", "pcub_polar_encode_bin",
            "pcub_sc_decode_qary_workspace", "pcub_sc_decode_qary", "pcub_polar_encode_qary",
-           "pcub_pack_bits", "pcub_unpack_bits", "pcub_transpose_pairs", "pcub_sc_deletion_supported",
+           "pcub_pack_bits", "pcub_unpack_bits", "pcub_transpose_pairs", "pcub_tile_pairs", "pcub_sc_deletion_supported",
            "pcub_sc_leaf_deletion_supported", "pcub_sc_decode_deletion", "pcub_sc_leaf_bin_workspace", "pcub_sc_leaf_bin", "pcub_sc_leaf_deletion",
            "pcub_sc_prior_bin_workspace", "pcub_sc_prior_bin",
            "pcub_sc_decode_qary_log_workspace", "pcub_sc_decode_qary_log",

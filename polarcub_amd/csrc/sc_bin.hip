@@ -18,17 +18,11 @@
 
 using namespace pcub;
 
-// A/B experiments (sc_bin_kx*.hip): kernels in their own namespaces, launched instead of the
-// tiled-root twin while pcub_sc_set_experiment(e) selects one.  Diagnostic hook, not the ABI.
-namespace pcubx1 { BinKernFn bin_kernel_x(int v, bool compact); }
-namespace pcubx2 { BinKernFn bin_kernel_x(int v, bool compact); }
-static BinKernFn exp_kernel(int e, int v, bool compact) {
-    switch (e) {
-        case 1: return pcubx1::bin_kernel_x(v, compact);
-        case 2: return pcubx2::bin_kernel_x(v, compact);
-        default: return nullptr;
-    }
-}
+// A/B experiments: a candidate kernel in its own translation unit and namespace (sc_bin_kx<e>.hip,
+// built with its own macros over the shared headers), launched instead of the tiled-root twin while
+// pcub_sc_set_experiment(e) selects it (scripts/ab_exp.py times both and compares their outputs).
+// Diagnostic hook, not the ABI; no experiment is built into the shipped library.
+static BinKernFn exp_kernel(int, int, bool) { return nullptr; }
 static int g_experiment = 0;
 extern "C" int pcub_sc_set_experiment(int e) {
     const int old = g_experiment;
@@ -60,7 +54,6 @@ KernFn variant_kernel(int v) {
     if (KernFn k = bin_kernel_part0(v)) return k;
     if (KernFn k = bin_kernel_part1(v)) return k;
     if (KernFn k = bin_kernel_part2(v)) return k;
-    if (KernFn k = bin_kernel_part3(v)) return k;
     if (KernFn k = bin_kernel_part4(v)) return k;
     return bin_kernel_part5(v);
 }
@@ -102,7 +95,8 @@ DevInfo dev_info() {
     if (hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return DevInfo{};
     for (int v = 0; v < kNumVariants; ++v) {
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, variant_kernel(v), kBlock, bin_lds_bytes(v)) != hipSuccess ||
+        const KernFn k = variant_kernel(v);
+        if (!k || hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kBlock, bin_lds_bytes(v)) != hipSuccess ||
             occ < 1)
             occ = 1;
         d.occ[v] = occ;
@@ -167,7 +161,7 @@ int pick_variant(int n) {
 
 }  // namespace
 
-extern "C" int pcub_abi_version(void) { return 2; }
+extern "C" int pcub_abi_version(void) { return 3; }
 
 // Tuning hooks (not part of the stable ABI): choose / describe the decode kernel variant.
 extern "C" int pcub_sc_num_variants(void) { return kNumVariants; }
@@ -198,7 +192,7 @@ extern "C" int pcub_sc_variant_for(int32_t log2N) {
     return pick_variant(log2N);
 }
 extern "C" int pcub_sc_set_variant(int v) {
-    if (v < 0 || v >= kNumVariants) return PCUB_EINVAL;
+    if (v < 0 || v >= kNumVariants || !variant_kernel(v)) return PCUB_EINVAL;  // not built: EINVAL
     g_variant = v;
     return 0;
 }

@@ -72,11 +72,13 @@ __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
 
 typedef void (*BinKernFn)(BinArgs);
 
-// The kernel of variant v if this translation unit instantiates it, else nullptr.
+// The kernel of variant v if this translation unit instantiates it, else nullptr.  The shipped library
+// builds the variants pick_variant can launch (0, 1, 10, 13, 14, 17, 24, 26, 31); the rest of kVar
+// are the round 1-3 sweep's geometries, measured slower, kept as table rows so the
+// variant numbers in profiles/ stay meaningful; pcub_sc_set_variant rejects them.
 BinKernFn bin_kernel_part0(int v);
 BinKernFn bin_kernel_part1(int v);
 BinKernFn bin_kernel_part2(int v);
-BinKernFn bin_kernel_part3(int v);
 BinKernFn bin_kernel_part4(int v);
 BinKernFn bin_kernel_part5(int v);
 // the compact-root twin of variant v (CR: root rows as compact normalised doubles), or nullptr

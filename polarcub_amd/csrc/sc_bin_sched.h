@@ -283,10 +283,6 @@ PCUB_HD uint64_t hl_frozen(uint64_t* ub, const uint64_t* fv, int j) {
     return ((uint64_t)((ym ^ yp) & SM)) | ((uint64_t)(yp & SM) << S);
 }
 
-#ifndef PCUB_R5
-#define PCUB_R5 0
-#endif
-
 // byte permute (v_perm_b32): result byte i = byte sel_i of the 8-byte value {hi, lo} (0..3: lo)
 PCUB_HD uint32_t perm_bytes(uint32_t hi, uint32_t lo, uint32_t sel) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -430,9 +426,7 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
     uint64_t acc = 0;
     int nacc = 0;
     int infow = 0;
-#if PCUB_R5
-    uint32_t acc32 = 0;
-#endif
+    uint32_t acc32 = 0;  // the packed path's accumulator (SUW >= 32)
 
     for (int k = 0; k < (1 << D); ++k) {
         if constexpr (TR) {
@@ -564,7 +558,6 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
             }
         }
         // information bits of this subtree, in u order (identical in all G lanes)
-#if PCUB_R5
         if constexpr (W::SUW >= 32) {
             // per 32-bit word of the window: the information bits packed by the precomputed compress
             // masks (all-frozen words skipped, all-information words taken whole), then appended
@@ -586,18 +579,19 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
                     nacc = (nacc + cnt) & 31;
                 }
             }
-        } else
-#endif
+        } else {
+            // windows narrower than a word (short codes): bit by bit
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            for (uint64_t im = ~fm[w] & W::WMASK; im != 0ull; im &= im - 1ull) {
-                const int q = __builtin_ctzll(im);
-                acc |= ((ub[w] >> q) & 1ull) << nacc;
-                if (++nacc == 32) {
-                    if (store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
-                    acc = 0;
-                    nacc = 0;
-                    ++infow;
+            for (int w = 0; w < NW; ++w) {
+                for (uint64_t im = ~fm[w] & W::WMASK; im != 0ull; im &= im - 1ull) {
+                    const int q = __builtin_ctzll(im);
+                    acc |= ((ub[w] >> q) & 1ull) << nacc;
+                    if (++nacc == 32) {
+                        if (store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
+                        acc = 0;
+                        nacc = 0;
+                        ++infow;
+                    }
                 }
             }
         }
@@ -619,32 +613,36 @@ PCUB_HD void decode_codeword(const BinArgs& A, long long cw, int j, int lane, lo
                 sty<YL>(base + (long long)w * ys, ldy<YL>(base + (long long)w * ys) ^ ldy<YL>(base + (long long)(w + Wc) * ys));
         }
     }
-#if PCUB_R5
     if constexpr (W::SUW >= 32) acc = acc32;
-#endif
     if (nacc && store && (infow & (G - 1)) == j) A.info[(long long)infow * B + cw] = (uint32_t)acc;
     // x_hat natural segment k = bitrev_g(j) is this lane's local Y, bit-reversed over nv bits
-#if PCUB_R5
     if (A.xhat && store && (nv == 8 || nv == 10)) {
         const int seg = (int)bitrev((uint32_t)j, g);
+        // the store pointer advances by B per word and is laundered each time, so the per-word
+        // addresses are not hoisted out of the tile loop (they were: 32 spilled 64-bit offsets)
+        uint32_t* xo = A.xhat + (long long)seg * (Nv >> 5) * B + cw;
         if (nv == 8) {
             uint32_t yw[8], o[8];
 #pragma unroll
             for (int w = 0; w < 8; ++w) yw[w] = ldy<YL>(Y + (long long)w * ys);
             xhat_r3(yw, o);
 #pragma unroll
-            for (int w = 0; w < 8; ++w) A.xhat[(long long)(seg * 8 + w) * B + cw] = o[w];
+            for (int w = 0; w < 8; ++w) {
+                stu(xo, o[w]);
+                xo = launder(xo + B);
+            }
         } else {
             uint32_t yw[32], o[32];
 #pragma unroll
             for (int r = 0; r < 32; ++r) yw[r] = ldy<YL>(Y + (long long)bitrev((uint32_t)r, 5) * ys);
             xhat_r5(yw, o);
 #pragma unroll
-            for (int w = 0; w < 32; ++w) A.xhat[(long long)(seg * 32 + w) * B + cw] = o[w];
+            for (int w = 0; w < 32; ++w) {
+                stu(xo, o[w]);
+                xo = launder(xo + B);
+            }
         }
-    } else
-#endif
-    if (A.xhat && store) {
+    } else if (A.xhat && store) {
         const int seg = (int)bitrev((uint32_t)j, g);
         const int W = Nv >> 5;
         for (int w = 0; w < W; ++w) {

@@ -56,10 +56,6 @@ PCUB_HD double cv_pack(double q, uint32_t s) {
     return from_bits(as_bits(q) | (long long)((unsigned long long)s << 63));
 }
 
-#ifndef PCUB_FAST_F
-#define PCUB_FAST_F 0
-#endif
-
 // RN(num / den) for the minus transform's normalisation: den = max(1 + ra*rb, ra + rb) in [1, 2]
 // (or NaN), num = the min in [0, 2].  The compiler's IEEE sequence without v_div_scale /
 // v_div_fixup: those only act near the ends of the exponent range (div_scale: a denominator or
@@ -107,11 +103,7 @@ PCUB_HD double op_f(double va, double vb) {
     // does; on a tie both are the same value.
     const double num = __builtin_fmin(p0, p1);
     const double den = __builtin_fmax(p0, p1);  // in [1, 2], or NaN
-#if PCUB_FAST_F
     return cv_pack(div_den12(num, den), a.s ^ b.s ^ (sw ? 1u : 0u));
-#else
-    return cv_pack(num / den, a.s ^ b.s ^ (sw ? 1u : 0u));
-#endif
 }
 
 // plus transform (BinaryMemorylessVectorDistribution.py:31-47) + normalise.
@@ -130,13 +122,9 @@ PCUB_HD double op_g(double va, double vb, uint32_t u) {
         const bool agt = a.r > b.r;
         const double mx = agt ? a.r : b.r;
         const double mn = agt ? b.r : a.r;
-#if PCUB_FAST_F
         // one comparison: where neither is greater the quotient is 1 (the tie (1, 1), either sign)
         // or NaN (the (0, 0) sentinel, either sign), so b.s ^ !agt is as good as b.r > a.r there
         s = b.s ^ (agt ? 0u : 1u);
-#else
-        s = b.s ? (agt ? 1u : 0u) : (b.r > a.r ? 1u : 0u);
-#endif
         q = mn / mx;
     }
     return cv_pack(q, s);

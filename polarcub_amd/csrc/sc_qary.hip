@@ -84,11 +84,18 @@ struct QGeom {
     int sr() const { return hl ? 2 * S : S; }
 };
 
-// LDS bytes of a workgroup's symbols: Nv/4 words per thread
-size_t qsym_lds_bytes(int n, int G) { return (size_t)kQBlock * ((((size_t)1 << n) / G + 3) / 4) * sizeof(uint32_t); }
+// symbols per 32-bit word (QPack): 16 two-bit fields at q = 4, else four bytes
+int qsym_per_word(int q) { return q == 4 ? 16 : 4; }
+// LDS bytes of a workgroup's symbols: ceil(Nv / per-word) words per thread
+size_t qsym_lds_bytes(int n, int G, int q) {
+    const size_t per = (size_t)qsym_per_word(q);
+    return (size_t)kQBlock * ((((size_t)1 << n) / G + per - 1) / per) * sizeof(uint32_t);
+}
 // LDS bytes of the split level's LDS half: S positions x q doubles per thread
 size_t qhl_lds_bytes(int q, int S) { return (size_t)kQBlock * S * q * sizeof(double); }
-constexpr int kQHlWaves = 3;  // the HL kernels' launch bounds
+// the HL kernels' launch bounds: four workgroups a CU (q = 4: 4 KB of 2-bit symbols + 32 KB of the
+// split level a workgroup), three for the byte-symbol alphabets
+int q_hl_waves(int q) { return q == 4 ? 4 : 3; }
 
 QGeom q_geom(int q, int n) {
     QGeom c{4, g_qlanes, false, false};  // 8 register positions (q <= 4) via pcub_sc_set_qary_regs
@@ -102,24 +109,24 @@ QGeom q_geom(int q, int n) {
     }
     // symbols in LDS while the resident workgroups' columns fit the CU's LDS (N <= 512 at G = 4)
     c.yl = g_qylds && qary_kernel_y(q, c.S, c.G) &&
-           (size_t)qary_waves(q, c.S, c.G) * qsym_lds_bytes(n, c.G) <= kQLdsPerCu;
+           (size_t)qary_waves(q, c.S, c.G) * qsym_lds_bytes(n, c.G, q) <= kQLdsPerCu;
     // the split level (with the symbols in LDS) where its three workgroups fit a CU and the code
     // has an outer level above it (N >= 4 S G)
     c.hl = c.yl && g_qhl && qary_kernel_h(q, c.S, c.G) && (1 << n) >= 4 * c.S * c.G &&
-           (size_t)kQHlWaves * (qsym_lds_bytes(n, c.G) + qhl_lds_bytes(q, c.S)) <= kQLdsPerCu;
+           (size_t)q_hl_waves(q) * (qsym_lds_bytes(n, c.G, q) + qhl_lds_bytes(q, c.S)) <= kQLdsPerCu;
     return c;
 }
 
 QKern qkernel(int q, int n, int* waves = nullptr) {
     const QGeom c = q_geom(q, n);
-    if (waves) *waves = c.hl ? kQHlWaves : qary_waves(q, c.S, c.G);
+    if (waves) *waves = c.hl ? q_hl_waves(q) : qary_waves(q, c.S, c.G);
     if (c.hl) return qary_kernel_h(q, c.S, c.G);
     return c.yl ? qary_kernel_y(q, c.S, c.G) : qary_kernel(q, c.S, c.G);
 }
 
 size_t qlaunch_lds(int q, int n) {
     const QGeom c = q_geom(q, n);
-    return (c.yl ? qsym_lds_bytes(n, c.G) : 0) + (c.hl ? qhl_lds_bytes(q, c.S) : 0);
+    return (c.yl ? qsym_lds_bytes(n, c.G, q) : 0) + (c.hl ? qhl_lds_bytes(q, c.S) : 0);
 }
 
 long long qgrid(long long B, int q, int n) {
@@ -148,7 +155,8 @@ long long qgrid(long long B, int q, int n) {
 size_t qslot_bytes(int n, int q) {
     const QGeom c = q_geom(q, n);
     const size_t Nv = ((size_t)1 << n) / c.G;
-    return (Nv - 2 * c.sr()) * (size_t)((q + 1) / 2) * sizeof(double2) + (c.yl ? 0 : ((Nv + 3) & ~(size_t)3));
+    const size_t per = (size_t)qsym_per_word(q);
+    return (Nv - 2 * c.sr()) * (size_t)((q + 1) / 2) * sizeof(double2) + (c.yl ? 0 : (Nv + per - 1) / per * 4);
 }
 
 int q_depth(int n, int q) {
@@ -201,7 +209,7 @@ int decode_qary_impl(const double* xy, int64_t B, int32_t log2N, int32_t q, int3
     A.info = info;
     A.xhat = xhat;
     A.nslots = g * kQBlock;
-    A.ylds_words = c.yl ? (int)(qsym_lds_bytes(log2N, c.G) / kQBlock / sizeof(uint32_t)) : 0;
+    A.ylds_words = c.yl ? (int)(qsym_lds_bytes(log2N, c.G, q) / kQBlock / sizeof(uint32_t)) : 0;
     A.tile = tile;
     char* slots = (char*)workspace + tb;
     A.scratch = (double2*)slots;

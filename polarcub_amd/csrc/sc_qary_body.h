@@ -22,7 +22,7 @@
 // with cross-lane exchanges.  The bottom S virtual positions of every chain live
 // in registers (QSub<S>); stage levels 1..D-1 in a per-slot scratch (q doubles per
 // position as ceil(q/2) 16-byte pairs, slot-minor, so a wave's access is one
-// contiguous run); re-encoded symbols one byte each, four to a 32-bit word.
+// contiguous run); re-encoded symbols in 32-bit words (QPack: 2-bit fields at q = 4, else bytes).
 //
 // Traffic.  Register subtree k is reached by a chain: one plus transform from
 // depth d0-1 (minus for k = 0), then minus transforms down to depth D.  A chain
@@ -160,33 +160,57 @@ struct QArgs {
     uint8_t* info;           // [K][B]
     uint8_t* xhat;           // [N][B] or null
     double2* scratch;        // [(N/G - 2S) positions][ceil(Q/2)][nslots]
-    uint32_t* ysym;          // [N/G/4 words][nslots], symbol of position p in byte p % 4 of word p / 4
+    uint32_t* ysym;          // [ceil(N/G/PER) words][nslots], symbol of position p in field p % PER of word p / PER
+                             // (QPack: PER = 16 2-bit fields at q = 4, else 4 bytes)
     long long nslots;
     int ylds_words;          // symbol words per thread in LDS (YL kernels; the HL column follows them)
     int tile;                // root layout: 0 = [N][B][Q]; T > 0 = [ceil(B/T)][N][T][Q] (T codewords a tile)
 };
 
-// Re-encoded symbols, four per word.  SWAR on bytes: every byte holds a value
-// < 2Q <= 16, so byte sums never carry, and (b | 0x80) - Q >= 0x78 never
-// borrows; its bit 7 is set iff b >= Q.
+// Re-encoded symbols packed into 32-bit words: q = 4 in 2-bit fields (16 a word: the C4 kernel's
+// column is 4 words a thread at N = 256, which lets four split-level workgroups share a CU's LDS),
+// every other q one byte each (four a word).
+template <int Q>
+struct QPack {
+    static constexpr int BITS = (Q == 4) ? 2 : 8;
+    static constexpr int PER = 32 / BITS;  // symbols per word
+    static constexpr uint32_t M = (1u << BITS) - 1u;
+};
+
+// SWAR on bytes: every byte holds a value < 2Q <= 16, so byte sums never carry, and
+// (b | 0x80) - Q >= 0x78 never borrows; its bit 7 is set iff b >= Q.
 template <int Q>
 PCUB_HD uint32_t q_mod_bytes(uint32_t s) {
     const uint32_t ge = (((s | 0x80808080u) - (uint32_t)Q * 0x01010101u) & 0x80808080u) >> 7;
     return s - ge * (uint32_t)Q;
 }
 
+// 2-bit fields: a + b mod 4 in every field (the low bits' sum carries into the high bit, the high
+// bits XOR; nothing crosses a field)
+PCUB_HD uint32_t add_mod4_fields(uint32_t a, uint32_t b) {
+    constexpr uint32_t H = 0xAAAAAAAAu;
+    return ((a & ~H) + (b & ~H)) ^ ((a ^ b) & H);
+}
+
 // parent = [(ym + yp) % Q | (Q - yp) % Q]  (QaryPolarEncoderDecoder.py:397-399, half-split order)
 template <int Q>
 PCUB_HD void q_combine_words(uint32_t& m, uint32_t& p) {
-    const uint32_t mm = q_mod_bytes<Q>(m + p);
-    p = q_mod_bytes<Q>((uint32_t)Q * 0x01010101u - p);
-    m = mm;
+    if constexpr (QPack<Q>::BITS == 2) {
+        const uint32_t mm = add_mod4_fields(m, p);
+        p = add_mod4_fields(~p, 0x55555555u);  // -p = ~p + 1 (mod 4) in every field
+        m = mm;
+    } else {
+        const uint32_t mm = q_mod_bytes<Q>(m + p);
+        p = q_mod_bytes<Q>((uint32_t)Q * 0x01010101u - p);
+        m = mm;
+    }
 }
 
 // YL: the symbols live in LDS (this thread's column, ldy/sty of sc_bin_body.h)
-template <bool YL = false>
+template <int Q, bool YL = false>
 PCUB_HD int q_sym(const uint32_t* Y, long long ns, int pos) {
-    return (int)((ldy<YL>(Y + (long long)(pos >> 2) * ns) >> ((pos & 3) * 8)) & 0xffu);
+    using P = QPack<Q>;
+    return (int)((ldy<YL>(Y + (long long)(pos / P::PER) * ns) >> ((pos % P::PER) * P::BITS)) & P::M);
 }
 
 // Decisions of the register subtree: information symbols go out in u order
@@ -346,7 +370,7 @@ struct QCol {
         if constexpr (E == 1) {
             const QV<Q> x0 = q_src<Q, ROOT>(P, c + M * C);
             const QV<Q> x1 = q_src<Q, ROOT>(P, c + (M + (1 << (F - 1))) * C);
-            if constexpr (GOP) v = q_plus<Q>(x0, x1, q_sym<YL>(P.Y, P.ys, P.ystart + c + M * C));
+            if constexpr (GOP) v = q_plus<Q>(x0, x1, q_sym<Q, YL>(P.Y, P.ys, P.ystart + c + M * C));
             else v = q_minus<Q>(x0, x1);
         } else {
             const QV<Q> l = QCol<Q, F, E - 1, M, GOP, ROOT, FINAL, YL>::run(P, c, C);
@@ -573,41 +597,45 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
 #pragma unroll
             for (int t = 0; t < SR; ++t) y[t] = 0;  // rate-0: symbols 0, re-encoding 0
         }
-        // the subtree's symbols into its words (SR < 4: a part of one word)
-        if constexpr (SR >= 4) {
+        // the subtree's symbols into its words (SR < PER: a part of one word)
+        constexpr int PER = QPack<Q>::PER, BITS = QPack<Q>::BITS;
+        if constexpr (SR >= PER) {
 #pragma unroll
-            for (int w = 0; w < SR / 4; ++w)
-                sty<YL>(Y + (long long)(k * SR / 4 + w) * ys, (uint32_t)y[4 * w] | ((uint32_t)y[4 * w + 1] << 8) |
-                                                              ((uint32_t)y[4 * w + 2] << 16) | ((uint32_t)y[4 * w + 3] << 24));
+            for (int w = 0; w < SR / PER; ++w) {
+                uint32_t ws = 0;
+#pragma unroll
+                for (int t = 0; t < PER; ++t) ws |= (uint32_t)y[PER * w + t] << (BITS * t);
+                sty<YL>(Y + (long long)(k * SR / PER + w) * ys, ws);
+            }
         } else {
-            uint32_t* yw = Y + (long long)((k * SR) >> 2) * ys;
-            const int sh = ((k * SR) & 3) * 8;
+            uint32_t* yw = Y + (long long)((k * SR) / PER) * ys;
+            const int sh = ((k * SR) % PER) * BITS;
             uint32_t ws = 0;
 #pragma unroll
-            for (int t = 0; t < SR; ++t) ws |= (uint32_t)y[t] << (8 * t);
+            for (int t = 0; t < SR; ++t) ws |= (uint32_t)y[t] << (BITS * t);
             sty<YL>(yw, (sh == 0 ? 0u : (ldy<YL>(yw) & ((1u << sh) - 1u))) | (ws << sh));
         }
         // combine completed plus children: [(ym+yp)%q | (q-yp)%q]
         for (int d = D; d >= 1 && ((k >> (D - d)) & 1); --d) {
             const int Lc = Nv >> d;
             const long long st = (long long)(k >> (D - d + 1)) * 2 * Lc;
-            if (Lc >= 4) {
-                for (int w = 0; w < Lc / 4; ++w) {
-                    uint32_t* pm = Y + (st / 4 + w) * ys;
-                    uint32_t* pp = Y + (st / 4 + Lc / 4 + w) * ys;
+            if (Lc >= PER) {
+                for (int w = 0; w < Lc / PER; ++w) {
+                    uint32_t* pm = Y + (st / PER + w) * ys;
+                    uint32_t* pp = Y + (st / PER + Lc / PER + w) * ys;
                     uint32_t m = ldy<YL>(pm), p = ldy<YL>(pp);
                     q_combine_words<Q>(m, p);
                     sty<YL>(pm, m);
                     sty<YL>(pp, p);
                 }
-            } else {  // Lc = 1, 2: the parent is 2 or 4 bytes of one word
-                uint32_t* pw = Y + (st >> 2) * ys;
-                const int sh = (int)(st & 3) * 8;
-                const uint32_t lm = (Lc == 1) ? 0xffu : 0xffffu;
+            } else {  // 2 Lc <= PER: the parent is 2 Lc fields of one word
+                uint32_t* pw = Y + (st / PER) * ys;
+                const int sh = (int)(st % PER) * BITS;
+                const uint32_t lm = (1u << (BITS * Lc)) - 1u;
                 const uint32_t w0 = ldy<YL>(pw);
-                uint32_t m = (w0 >> sh) & lm, p = (w0 >> (sh + 8 * Lc)) & lm;
+                uint32_t m = (w0 >> sh) & lm, p = (w0 >> (sh + BITS * Lc)) & lm;
                 q_combine_words<Q>(m, p);
-                sty<YL>(pw, (w0 & ~(((lm << (8 * Lc)) | lm) << sh)) | (((p << (8 * Lc)) | m) << sh));
+                sty<YL>(pw, (w0 & ~(((lm << (BITS * Lc)) | lm) << sh)) | ((((p & lm) << (BITS * Lc)) | (m & lm)) << sh));
             }
         }
     }
@@ -615,7 +643,7 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
     // bitrev_n(j) + bitrev_{nv}(t), t = its local position
     if (A.xhat && store) {
         uint8_t* xo = A.xhat + cw + (long long)bitrev((uint32_t)j, A.n) * A.B;
-        for (int t = 0; t < Nv; ++t) xo[(long long)bitrev((uint32_t)t, nv) * A.B] = (uint8_t)q_sym<YL>(Y, ys, t);
+        for (int t = 0; t < Nv; ++t) xo[(long long)bitrev((uint32_t)t, nv) * A.B] = (uint8_t)q_sym<Q, YL>(Y, ys, t);
     }
 }
 

@@ -19,22 +19,22 @@ QKern qary_kernel_q4(int S, int G) {
     return qary_kernel_geom<4, 8>(S, G);
 }
 
-// the C4 geometry with its symbols in LDS (16 words a thread at N = 256)
+// the C4 geometry with its symbols in LDS (4 words of 2-bit symbols a thread at N = 256)
 QKern qary_kernel_q4_y(int S, int G) {
     if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, qary_waves(4, 4, 4), 1, true>;
     return nullptr;
 }
 
-// the split-level twin: 2S = 8 positions per lane at a chain's end, 4 of them in LDS (48 KB a
-// workgroup with the symbols, three workgroups a CU)
+// the split-level twin: 2S = 8 positions per lane at a chain's end, 4 of them in LDS (36 KB a
+// workgroup with the 2-bit symbols, four workgroups a CU: at most 128 VGPRs)
 QKern qary_kernel_q4_h(int S, int G) {
-    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 3, 1, true, true>;
+    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 4, 1, true, true>;
     return nullptr;
 }
 
 // ... reading its root rows in the wave's own tiles (TR: tile = 16, a wave-uniform base)
 QKern qary_kernel_q4_h_tr(int S, int G) {
-    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 3, 1, true, true, true>;
+    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 4, 1, true, true, true>;
     return nullptr;
 }
 

@@ -179,7 +179,43 @@ __global__ __launch_bounds__(256) void k_transpose(const double* __restrict__ sr
     }
 }
 
+// [B][N][q] -> the tiled root layout [ceil(B/T)][N][T][q] (codeword b's row i at ((b / T) N + i) T +
+// b % T; the padding columns of the last tile zero) through the same 32 x 16 LDS tile: the reference
+// API's per-codeword rows straight into the layout the decode kernels read one wave-block at a time.
+__global__ __launch_bounds__(256) void k_tile_pairs(const double* __restrict__ src, long long B, long long Bp, int N,
+                                                   int q, int T, double* __restrict__ dst) {
+    __shared__ double tile[32][16 * 8 + 1];
+    const long long b0 = (long long)blockIdx.x * 32;
+    const int i0 = blockIdx.y * 16;
+    const int t = threadIdx.x;
+    for (int e = t; e < 32 * 16 * q; e += 256) {
+        const int r = e / (16 * q), c = e % (16 * q);
+        const long long b = b0 + r;
+        const int i = i0 + c / q;
+        if (i < N) tile[r][c] = b < B ? src[(b * N + i0) * q + c] : 0.0;
+    }
+    __syncthreads();
+    for (int e = t; e < 16 * 32 * q; e += 256) {
+        const int ii = e / (32 * q), c = e % (32 * q);
+        const int r = c / q, x = c % q;
+        const long long b = b0 + r;
+        const int i = i0 + ii;
+        if (b < Bp && i < N) dst[(((b / T) * N + i) * T + b % T) * q + x] = tile[r][ii * q + x];
+    }
+}
+
 }  // namespace
+
+extern "C" int pcub_tile_pairs(const double* src, int64_t B, int32_t N, int32_t q, int32_t T, double* dst,
+                               void* stream) {
+    if (B < 0 || N < 0 || q < 1 || q > 8 || T < 1 || T > 4096 || (B > 0 && N > 0 && (!src || !dst))) return PCUB_EINVAL;
+    if (B == 0 || N == 0) return 0;
+    const long long Bp = (B + T - 1) / T * T;
+    if (((Bp + 31) / 32) * 256 > 0xffffffffLL || ((N + 15) / 16) > 65535) return PCUB_EINVAL;
+    const dim3 grid((unsigned)((Bp + 31) / 32), (unsigned)((N + 15) / 16));
+    hipLaunchKernelGGL(k_tile_pairs, grid, dim3(256), 0, (hipStream_t)stream, src, (long long)B, Bp, N, q, T, dst);
+    return (int)hipGetLastError();
+}
 
 extern "C" int pcub_polar_encode_bin(const uint32_t* info_words, int64_t B, int32_t log2N, const uint32_t* frozen_mask,
                                      const uint32_t* frozen_val, int32_t K, uint32_t* x_words, void* stream) {

@@ -283,9 +283,12 @@ class BinaryDecoder:
 
     def decode(self, xy):
         """xy: [B, N, 2] float64 (per-codeword rows, as the reference's probs).
-        Returns (info [B, K] uint8, xhat [B, N] uint8)."""
-        native = transpose_pairs(xy)
-        info_w, xh_w, _ = self.decode_native(native)
+        Returns (info [B, K] uint8, xhat [B, N] uint8).  The rows go in one pass into the tiled root
+        layout (pcub_tile_pairs) and through the headline kernel (decode_tiled_native); the same
+        decisions as decode_native on the transposed rows."""
+        B = xy.shape[0]
+        T = bin_tile(self.code.n)
+        info_w, xh_w, _ = self.decode_tiled_native(tile_pairs(xy, T), B)
         return unpack(info_w, self.code.K), unpack(xh_w, self.code.N)
 
 
@@ -414,6 +417,18 @@ def transpose_pairs(xy):
     return out
 
 
+def tile_pairs(xy, T):
+    """[B, N, q] float64 on device -> the tiled layout [ceil(B/T), N, T, q] (pcub_tile_pairs; padding
+    columns zero): the same array as tile_rows(transpose_pairs(xy), T) in one pass."""
+    if xy.dtype != torch.float64 or xy.dim() != 3:
+        raise ValueError("expected float64 [B, N, q]")
+    xy = xy.contiguous()
+    B, N, q = xy.shape
+    out = torch.empty(((B + T - 1) // T, N, T, q), dtype=torch.float64, device=xy.device)
+    _lib.check(_lib.lib().pcub_tile_pairs(_p(xy), B, N, q, int(T), _p(out), _stream()), "pcub_tile_pairs")
+    return out
+
+
 def unpack(words, nbits):
     """[W, B] int32 words -> [B, nbits] uint8 on device."""
     W, B = words.shape
@@ -526,8 +541,10 @@ class QaryDecoder:
         return info[:c.K], xh
 
     def decode(self, xy):
-        """xy: [B, N, q] float64 -> (info [B, K] uint8, xhat [B, N] uint8)."""
-        info, xh = self.decode_native(transpose_pairs(xy))
+        """xy: [B, N, q] float64 -> (info [B, K] uint8, xhat [B, N] uint8), through the tiled layout
+        (pcub_tile_pairs, decode_tiled_native)."""
+        B = xy.shape[0]
+        info, xh = self.decode_tiled_native(tile_pairs(xy, self.tile()), B)
         return info.t().contiguous(), xh.t().contiguous()
 
 

@@ -14,6 +14,7 @@ ap.add_argument("--n", type=int, default=10)
 ap.add_argument("--batch", type=int, default=1 << 20)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--variant", type=int, default=None)
+ap.add_argument("--exp", type=int, default=0, help="pcub_sc_set_experiment (A/B kernels, sc_bin_kx*.hip)")
 ap.add_argument("--no-tile", action="store_true", help="root rows [N][B][2] instead of the kernel's tiles (bench.py)")
 a = ap.parse_args()
 N = 1 << a.n
@@ -22,6 +23,11 @@ s2 = construction.awgn_sigma2(2.0, 0.5)
 fr = construction.bhattacharyya_frozen(a.n, K, s2)
 code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(fr)[0].tolist()), 1)
 sc.set_variant(a.variant)
+if a.exp:
+    import ctypes
+    from polarcub_amd import _lib
+    _lib.lib().pcub_sc_set_experiment.argtypes = [ctypes.c_int]
+    _lib.lib().pcub_sc_set_experiment(a.exp)
 dec = sc.BinaryDecoder(code)
 gen = torch.Generator(device="cuda")
 gen.manual_seed(1)

@@ -36,7 +36,7 @@ static int run(const double* xy, long long B, int n, const uint8_t* frozen, uint
     std::vector<uint8_t> ef((size_t)1 << D);
     for (int k = 0; k < (1 << D); ++k) ef[k] = (uint8_t)first_frozen_depth(words.data(), k, D, SR);
     std::vector<double2> scr((size_t)(N - 2 * SR) * ((Q + 1) / 2) * ns + 1);
-    std::vector<uint32_t> ys((size_t)(N + 3) / 4 * ns);
+    std::vector<uint32_t> ys((size_t)(N + 3) / 4 * ns);  // bytes' worth: enough for every QPack
     QArgs A;
     A.xy = xy;
     A.B = B;

@@ -34,7 +34,19 @@ def test_library_exports_every_declared_symbol():
     H = ctypes.CDLL(build.HOST_LIB)  # host-only construction library (include/polarcub_construct.h)
     missing = [n for n in sorted(_declared("polarcub_construct.h")) if not hasattr(H, n)]
     assert not missing, missing
-    assert _lib.lib().pcub_abi_version() == _lib.ABI_VERSION == 2
+    assert _lib.lib().pcub_abi_version() == _lib.ABI_VERSION == 3
+
+
+def test_built_variants_are_the_launchable_ones():
+    """The library builds the binary variants pick_variant can launch and no other (host-only calls)."""
+    from polarcub_amd import _lib
+    from tests.test_gpu_decode import VARIANTS
+    L = _lib.lib()
+    built = [v for v in range(L.pcub_sc_num_variants()) if L.pcub_sc_set_variant(v) == 0]
+    L.pcub_sc_set_variant(L.pcub_sc_default_variant())
+    assert built == VARIANTS
+    for n in range(6, 17):
+        assert L.pcub_sc_variant_for(n) in VARIANTS
 
 
 def test_invalid_arguments_are_rejected_without_touching_the_device():
@@ -45,6 +57,8 @@ def test_invalid_arguments_are_rejected_without_touching_the_device():
     assert L.pcub_sc_decode_qary(None, 1, 8, 9, None, 0, None, None, None, 0, None) == _lib.EINVAL
     assert L.pcub_polar_encode_bin(None, 1, 40, None, None, 0, None, None) == _lib.EINVAL
     assert L.pcub_transpose_pairs(None, 4, 4, 9, None, None) == _lib.EINVAL
+    assert L.pcub_tile_pairs(None, 4, 4, 2, 0, None, None) == _lib.EINVAL
+    assert L.pcub_tile_pairs(None, 4, 4, 2, 16, None, None) == _lib.EINVAL
     assert L.pcub_sc_decode_bin_workspace(0, 10) == 0
     # segment-state tables: sizes, argument checks, and the layout query (host-only code paths)
     assert L.pcub_sc_deletion_table_bytes(2) == (8 + 32 * 16) * 8  # header (magic, n0, pd) + rows

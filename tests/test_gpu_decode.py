@@ -9,7 +9,9 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 BIN_SETS = ["bsc_n64", "awgn_n1024", "awgn_n4096", "awgn_n256_lowsnr"]
-NVAR = 33  # kernel variants (sc_bin_kern.h); 24-30 and 32 keep the re-encoded bits in LDS, 26-28 and 30-32 split their last level (LDS + registers)
+# the kernel variants the library builds (sc_bin_kern.h; the ones pick_variant can launch): 24 and 26
+# keep the re-encoded bits in LDS, 26 and 31 split their last level (LDS + registers)
+VARIANTS = [0, 1, 10, 13, 14, 17, 24, 26, 31]
 
 
 def _xy(g):
@@ -22,7 +24,7 @@ def sc():
     return _sc
 
 
-@pytest.mark.parametrize("variant", range(NVAR))
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("name", BIN_SETS)
 def test_decode_matches_reference(sc, name, variant):
     sc.set_variant(variant)
@@ -37,7 +39,7 @@ def test_decode_matches_reference(sc, name, variant):
     sc.set_variant()
 
 
-@pytest.mark.parametrize("variant", [0, 3, 6, 9, 11, 24])
+@pytest.mark.parametrize("variant", [0, 1, 10, 13, 14, 24])
 @pytest.mark.parametrize("idx", range(24))
 def test_edge_cases(sc, idx, variant):
     sc.set_variant(variant)
@@ -49,7 +51,7 @@ def test_edge_cases(sc, idx, variant):
     assert np.array_equal(xhat.cpu().numpy(), c["xhat"])
 
 
-@pytest.mark.parametrize("variant", range(NVAR))
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_ragged_batches_and_slot_reuse(sc, variant):
     """Batch sizes that are not tile multiples, and more tiles than resident slots."""
     from oracle import orc
@@ -70,7 +72,7 @@ def test_ragged_batches_and_slot_reuse(sc, variant):
     sc.set_variant()
 
 
-@pytest.mark.parametrize("variant", range(NVAR))
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_rate0_blocks(sc, variant):
     """Frozen sets full of aligned rate-0 blocks (skipped by every variant's schedule,
     at the stage levels and inside the register and cross-lane subtrees)."""
@@ -118,7 +120,7 @@ def test_decode_then_reencode_roundtrip_large(sc):
     assert torch.equal(dx, x)
 
 
-@pytest.mark.parametrize("variant", [0, 7, 17, 24, 26, 31])
+@pytest.mark.parametrize("variant", [0, 1, 17, 24, 26, 31])
 def test_tiled_root_layout(sc, variant):
     """pcub_sc_decode_bin_tiled: the root rows in tiles of T codewords ([ceil(B/T), N, T, 2], the
     kernel's own wave width and others, ragged last tiles) decode exactly as the [N, B, 2] rows, for

@@ -146,3 +146,39 @@ def test_long_code_encode_matches_oracle(n):
     cnt = mc.run_bin(code, 5, 0, 96, mc.CHANNEL_BSC, 0.0, chunk=64)  # noiseless: every word decodes
     torch.cuda.synchronize()
     assert cnt[0] == 96 and cnt[1] == 0 and cnt[2] == 0
+
+
+@pytest.mark.parametrize("n,B", [(4, 37), (6, 100), (10, 1000), (10, 16), (12, 77)])
+def test_batch_decode_through_tiles_matches_native(n, B):
+    """BinaryDecoder.decode ([B, N, 2], the reference API's layout) goes through pcub_tile_pairs and
+    the tiled headline kernel: the same decisions as the untiled kernel on the transposed rows, and
+    tile_pairs is the two-pass tile_rows(transpose_pairs(.)) in one pass."""
+    import torch
+    from polarcub_amd import construction, sc
+    N, K = 1 << n, (1 << n) // 2
+    s2 = construction.awgn_sigma2(2.0, 0.5)
+    fr = construction.bhattacharyya_frozen(n, K, s2)
+    code = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(fr)[0].tolist()), 1, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(n * 1000 + B)
+    xy = torch.rand((B, N, 2), dtype=torch.float64, device="cuda", generator=g)
+    T = sc.bin_tile(n)
+    assert torch.equal(sc.tile_pairs(xy, T), sc.tile_rows(sc.transpose_pairs(xy), T))
+    dec = sc.BinaryDecoder(code)
+    info, xh = dec.decode(xy)
+    iw, xw, _ = dec.decode_native(sc.transpose_pairs(xy))
+    assert torch.equal(info, sc.unpack(iw, K)) and torch.equal(xh, sc.unpack(xw, N))
+
+
+def test_qary_batch_decode_through_tiles_matches_native():
+    import torch
+    from polarcub_amd import sc
+    q, n, B = 4, 8, 333
+    rng = np.random.default_rng(5)
+    mask = (rng.random(1 << n) < 0.5).astype(np.uint8)
+    code = sc.QaryCode(q, 1 << n, mask, device="cuda")
+    xy = torch.as_tensor(rng.random((B, 1 << n, q)), device="cuda")
+    dec = sc.QaryDecoder(code)
+    info, xh = dec.decode(xy)
+    i2, x2 = dec.decode_native(sc.transpose_pairs(xy))
+    assert torch.equal(info, i2.t().contiguous()) and torch.equal(xh, x2.t().contiguous())

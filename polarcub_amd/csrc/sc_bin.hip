@@ -18,11 +18,15 @@
 
 using namespace pcub;
 
-// A/B experiments: a candidate kernel in its own translation unit and namespace (sc_bin_kx<e>.hip,
-// built with its own macros over the shared headers), launched instead of the tiled-root twin while
-// pcub_sc_set_experiment(e) selects it (scripts/ab_exp.py times both and compares their outputs).
-// Diagnostic hook, not the ABI; no experiment is built into the shipped library.
-static BinKernFn exp_kernel(int, int, bool) { return nullptr; }
+// A/B experiments: a candidate kernel compiled outside the library build (its own translation unit,
+// namespace and header copies; scripts/exp_build.sh) and linked in as pcub_exp_kernel, launched
+// instead of the tiled-root twin while pcub_sc_set_experiment(e) selects it (scripts/ab_exp.py times
+// both and compares their outputs).  Diagnostic hook, not the ABI: the shipped library has no
+// pcub_exp_kernel (a weak reference, null), so the hook launches nothing.
+extern "C" __attribute__((weak)) void* pcub_exp_kernel(int e, int v, int compact);
+static BinKernFn exp_kernel(int e, int v, bool compact) {
+    return pcub_exp_kernel ? (BinKernFn)pcub_exp_kernel(e, v, compact ? 1 : 0) : nullptr;
+}
 static int g_experiment = 0;
 extern "C" int pcub_sc_set_experiment(int e) {
     const int old = g_experiment;

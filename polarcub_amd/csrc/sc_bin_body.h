@@ -133,9 +133,10 @@ PCUB_HD unsigned dpp32(unsigned old, unsigned src) {
 
 template <int MASK>
 PCUB_HD unsigned xor_lane32(unsigned x) {
-    if constexpr (MASK == 1) return dpp32<0xB1>(0u, x);         // quad_perm [1,0,3,2]
-    else if constexpr (MASK == 2) return dpp32<0x4E>(0u, x);    // quad_perm [2,3,0,1]
-    else if constexpr (MASK == 8) return dpp32<0x128>(0u, x);   // row_ror:8
+    // every lane is written (all rows and banks, no bound_ctrl): no old value to materialise
+    if constexpr (MASK == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+    else if constexpr (MASK == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+    else if constexpr (MASK == 8) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);
     else return dpp32<0x124, 0xA>(dpp32<0x12C>(0u, x), x);      // row_ror:12, banks 1,3: row_ror:4
 }
 
@@ -163,12 +164,11 @@ struct XSub {
     static PCUB_HD uint32_t run(double v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane) {
         const double w = xor_shfl_c<M / 2>(v);
         const bool lo = (lane & (M / 2)) == 0;
-        const double a = lo ? v : w, b = lo ? w : v;
         if constexpr (M == 2) {
             // both leaves of the pair from one product, u1's decision for either u0 (no branch:
             // leaf_g's if/else compiled to an exec-masked region; 75.0 -> 78.1 M cw/s at C2)
             uint32_t d0, d10, d11;
-            leaf_pair(a, b, d0, d10, d11);
+            leaf_pair_x(v, w, lo, d0, d10, d11);
             const uint32_t u0 = ((fm >> UBASE) & 1u) ? (uint32_t)((fv >> UBASE) & 1u) : d0;
             const uint32_t u1 = ((fm >> (UBASE + 1)) & 1u) ? (uint32_t)((fv >> (UBASE + 1)) & 1u) : (u0 ? d11 : d10);
             ub |= ((uint64_t)u0 << UBASE) | ((uint64_t)u1 << (UBASE + 1));
@@ -184,13 +184,13 @@ struct XSub {
                 ym = frozen_local<1, H>(fv >> UBASE, pos) & 1u;
                 ub |= fv & (HM << UBASE);
             } else {
-                ym = XSub<H, UBASE>::run(op_f(a, b), ub, fm, fv, lane);
+                ym = XSub<H, UBASE>::run(op_f(v, w), ub, fm, fv, lane);
             }
             if (all_frozen<H>(fm, UBASE + H)) {
                 yp = frozen_local<1, H>(fv >> (UBASE + H), pos) & 1u;
                 ub |= fv & (HM << (UBASE + H));
             } else {
-                yp = XSub<H, UBASE + H>::run(op_g(a, b, ym), ub, fm, fv, lane);
+                yp = XSub<H, UBASE + H>::run(op_g_x(v, w, lo, ym), ub, fm, fv, lane);
             }
             return lo ? (ym ^ yp) : yp;
         }

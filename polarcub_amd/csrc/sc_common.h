@@ -89,21 +89,29 @@ PCUB_HD double norm_pack(double p0, double p1) {
     return cv_pack(num / den, sw ? 1u : 0u);
 }
 
+// high word of a double, and q with its high word replaced: the orientation bookkeeping below works on
+// the sign bits in place (v_xor3 / v_and_or on the high words; round 5, 89.6 -> 90.4 M cw/s at C2)
+PCUB_HD uint32_t hi32(double v) { return (uint32_t)((unsigned long long)as_bits(v) >> 32); }
+PCUB_HD double with_hi(double q, uint32_t hi) {
+    return from_bits((long long)(((unsigned long long)hi << 32) | ((unsigned long long)as_bits(q) & 0xffffffffull)));
+}
+
 // minus transform (BinaryMemorylessVectorDistribution.py:15-29) + normalise,
 // on compact inputs a = row 2h, b = row 2h+1.
 //   canonical:  p0 = 1*1 + ra*rb,  p1 = 1*rb + ra*1
+// Symmetric in (a, b): every term commutes and the orientation is a.s ^ b.s ^ sw, so the cross-lane
+// leaves call it on (own, partner) without selecting which is row 2h.
 PCUB_HD double op_f(double va, double vb) {
-    const CV a = cv_load(va), b = cv_load(vb);
-    const double m = a.r * b.r;
+    const double ar = __builtin_fabs(va), br = __builtin_fabs(vb);
+    const double m = ar * br;
     const double p0 = 1.0 + m;
-    const double p1 = a.r + b.r;
+    const double p1 = ar + br;
     const bool sw = p1 > p0;
-    // p0 and p1 are both NaN (an input is the (0, 0) sentinel) or both numbers,
-    // so minNum/maxNum (v_min_f64 / v_max_f64) select exactly what the compare
-    // does; on a tie both are the same value.
     const double num = __builtin_fmin(p0, p1);
-    const double den = __builtin_fmax(p0, p1);  // in [1, 2], or NaN
-    return cv_pack(div_den12(num, den), a.s ^ b.s ^ (sw ? 1u : 0u));
+    const double den = __builtin_fmax(p0, p1);
+    const double q = div_den12(num, den);
+    const uint32_t hs = (hi32(va) ^ hi32(vb) ^ (sw ? 0x80000000u : 0u)) & 0x80000000u;
+    return with_hi(q, hi32(q) | hs);
 }
 
 // plus transform (BinaryMemorylessVectorDistribution.py:31-47) + normalise.
@@ -112,22 +120,58 @@ PCUB_HD double op_f(double va, double vb) {
 // normalised ratio is min/max.  (The if/else stays a branch: when every lane of the wave has the
 // same orientation the division is skipped, which a select-based form measured 8 % slower for.)
 PCUB_HD double op_g(double va, double vb, uint32_t u) {
-    const CV a = cv_load(va), b = cv_load(vb);
-    // the same-orientation result for every lane (one multiply), the opposite-orientation lanes
-    // overwrite it in a one-sided branch (no else region: two exec-mask instructions fewer)
-    double q = a.r * b.r;
-    uint32_t s = b.s;
-    if ((a.s ^ u) != b.s) {
-        // a NaN lands in mn (a) or mx (b) and the quotient is NaN; 0/0 is the (0, 0) output
-        const bool agt = a.r > b.r;
-        const double mx = agt ? a.r : b.r;
-        const double mn = agt ? b.r : a.r;
-        // one comparison: where neither is greater the quotient is 1 (the tie (1, 1), either sign)
-        // or NaN (the (0, 0) sentinel, either sign), so b.s ^ !agt is as good as b.r > a.r there
-        s = b.s ^ (agt ? 0u : 1u);
+    const double ar = __builtin_fabs(va), br = __builtin_fabs(vb);
+    const uint32_t sb = hi32(vb) & 0x80000000u;
+    double q = ar * br;
+    uint32_t s = sb;
+    if ((int32_t)(hi32(va) ^ hi32(vb) ^ (u << 31)) < 0) {
+        const bool agt = ar > br;
+        const double mx = agt ? ar : br;
+        const double mn = agt ? br : ar;
+        s = sb ^ (agt ? 0u : 0x80000000u);
         q = mn / mx;
     }
-    return cv_pack(q, s);
+    return with_hi(q, hi32(q) | s);
+}
+
+// The cross-lane forms: this lane holds v, its partner w, and lo says whether v is the pair's first
+// row (a = lo ? v : w, b = lo ? w : v).  The products, sums, min / max and orientation tests are
+// symmetric in (a, b), so only single bits are selected by lo, not the doubles (XSub; with the
+// symmetric op_f and DPP moves without an old operand, 90.4 -> 92.2 M cw/s at C2).  Same values as
+// op_g(a, b, u) / leaf_pair(a, b) bit for bit (a NaN operand may surface as another NaN: either is
+// the (0, 0) sentinel).
+PCUB_HD double op_g_x(double v, double w, bool lo, uint32_t u) {
+    const double vr = __builtin_fabs(v), wr = __builtin_fabs(w);
+    const uint32_t sv = hi32(v) & 0x80000000u, sw_ = hi32(w) & 0x80000000u;
+    const uint32_t sb = lo ? sw_ : sv;
+    double q = vr * wr;
+    uint32_t s = sb;
+    if ((int32_t)(hi32(v) ^ hi32(w) ^ (u << 31)) < 0) {
+        const bool gvw = vr > wr, gwv = wr > vr;
+        const bool agt = lo ? gvw : gwv;
+        const double mx = gvw ? vr : wr;
+        const double mn = gvw ? wr : vr;
+        s = sb ^ (agt ? 0u : 0x80000000u);
+        q = mn / mx;
+    }
+    return with_hi(q, hi32(q) | s);
+}
+
+PCUB_HD void leaf_pair_x(double v, double w, bool lo, uint32_t& d0, uint32_t& d1u0, uint32_t& d1u1) {
+    const double vr = __builtin_fabs(v), wr = __builtin_fabs(w);
+    const bool vs = (int32_t)hi32(v) < 0, ws = (int32_t)hi32(w) < 0;
+    const double m = vr * wr;
+    const double p0 = 1.0 + m;
+    const double p1 = vr + wr;
+    const bool diff = vs != ws;
+    d0 = (diff ? (p0 > p1) : (p1 > p0)) ? 1u : 0u;
+    const bool bs = lo ? ws : vs;
+    const bool agt = lo ? (vr > wr) : (wr > vr);
+    const bool bgt = lo ? (wr > vr) : (vr > wr);
+    const uint32_t ds = (bs && (m < 1.0)) ? 1u : 0u;
+    const uint32_t dd = (bs ? agt : bgt) ? 1u : 0u;
+    d1u0 = diff ? dd : ds;
+    d1u1 = diff ? ds : dd;
 }
 
 // Leaf pair (a, b) = rows (2h, 2h+1) of a length-2 node: u0's decision (leaf_f) and u1's

@@ -93,9 +93,9 @@ size_t qsym_lds_bytes(int n, int G, int q) {
 }
 // LDS bytes of the split level's LDS half: S positions x q doubles per thread
 size_t qhl_lds_bytes(int q, int S) { return (size_t)kQBlock * S * q * sizeof(double); }
-// the HL kernels' launch bounds: four workgroups a CU (q = 4: 4 KB of 2-bit symbols + 32 KB of the
-// split level a workgroup), three for the byte-symbol alphabets
-int q_hl_waves(int q) { return q == 4 ? 4 : 3; }
+// the HL kernels' launch bounds: three workgroups a CU (q = 4: 4 KB of 2-bit symbols + 32 KB of the
+// split level a workgroup would let four share the LDS, but the registers allow three)
+int q_hl_waves(int) { return 3; }
 
 QGeom q_geom(int q, int n) {
     QGeom c{4, g_qlanes, false, false};  // 8 register positions (q <= 4) via pcub_sc_set_qary_regs

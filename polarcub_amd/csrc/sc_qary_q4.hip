@@ -26,15 +26,16 @@ QKern qary_kernel_q4_y(int S, int G) {
 }
 
 // the split-level twin: 2S = 8 positions per lane at a chain's end, 4 of them in LDS (36 KB a
-// workgroup with the 2-bit symbols, four workgroups a CU: at most 128 VGPRs)
+// workgroup with the 2-bit symbols; three workgroups a CU: the kernel needs ~168 VGPRs, and at the
+// 128 of four workgroups it spilled 119 VGPRs and ran 2 % slower, 88.3 vs 90.0 M cw/s)
 QKern qary_kernel_q4_h(int S, int G) {
-    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 4, 1, true, true>;
+    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 3, 1, true, true>;
     return nullptr;
 }
 
 // ... reading its root rows in the wave's own tiles (TR: tile = 16, a wave-uniform base)
 QKern qary_kernel_q4_h_tr(int S, int G) {
-    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 4, 1, true, true, true>;
+    if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 3, 1, true, true, true>;
     return nullptr;
 }
 

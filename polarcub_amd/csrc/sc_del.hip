@@ -190,7 +190,9 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     // bit-packed received words in LDS when the group's words fit in 32 KiB (always for
     // the 64-trellis shapes; very long padded rows of small codes parse from HBM)
     A.rw = (dense || cpb * rw * 4 <= 32768) ? (int)rw : 0;
-    const size_t lds = A.rw ? (size_t)(cpb * rw * 4) : 0;
+    size_t lds = A.rw ? (size_t)(cpb * rw * 4) : 0;
+    // the table-driven kernel's staging area for its group's raw rows (sc_del_dense.h)
+    if (dense && dense_stage_bytes(stride, rx)) lds = (size_t)(dense_stage_off((int)rw) * 4 + dense_stage_bytes(stride, rx));
     // n0 = 2 without ones (and the table-driven layout): each workgroup first builds or copies the
     // segment-state table, so the launch is persistent
     if (dense || (n0 == 2 && ones == 0)) grid = resident_grid(k, lds, grid);
@@ -206,7 +208,9 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     const DelKern fk = fb_dense ? del_kernel_dense(2, n - n0, false) : kern;
     const long long fcpb = fb_dense ? kDenseCPB : kDelBlock >> (n - n0);
     F.rw = (fb_dense || fcpb * rw * 4 <= 32768) ? (int)rw : 0;
-    const size_t flds = F.rw ? (size_t)(fcpb * rw * 4) : 0;
+    size_t flds = F.rw ? (size_t)(fcpb * rw * 4) : 0;
+    if (fb_dense && dense_stage_bytes(stride, rx))
+        flds = (size_t)(dense_stage_off((int)rw) * 4 + dense_stage_bytes(stride, rx));
     const long long fgrid = resident_grid(fk, flds, (B + fcpb - 1) / fcpb);
     hipLaunchKernelGGL(fk, dim3((unsigned)fgrid), dim3(kDelBlock), flds, (hipStream_t)stream, F);
     return (int)hipGetLastError();

@@ -99,6 +99,62 @@ PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, i
     }
 }
 
+// Staged received words (round 5): a group's kDenseCPB rows are one contiguous run of CPB * stride
+// bytes (16-byte aligned when the batch is: CPB = 16), so the workgroup reads them with 16-byte
+// loads, every lane one or two, into an LDS staging area, and the waves bit-pack their rows from
+// there; pack_rows' byte loads cost a VMEM instruction and a ballot per 64 symbols of every row
+// (12 dependent-latency loads per C5 codeword).  The launcher sizes the LDS (dense_stage_bytes) and
+// the kernel stages whenever that size is nonzero.
+constexpr int kDenseStageMax = 24 * 1024;  // staging bytes per workgroup, at most
+
+PCUB_HD long long dense_stage_bytes(int stride, const void* rx) {
+    const long long b = (long long)kDenseCPB * stride;
+    return (b <= kDenseStageMax && ((unsigned long long)rx & 15ull) == 0) ? b : 0;
+}
+
+// the staging area: after the packed rows, 16-byte aligned
+PCUB_HD long long dense_stage_off(int rw) { return (((long long)kDenseCPB * rw + 3) / 4) * 4; }
+
+__device__ __forceinline__ void stage_rows(const DelArgs& A, long long grp, uint8_t* stg, int nb) {
+    const long long total = A.B * (long long)A.stride;  // bytes of the batch's rows
+    const long long g0 = grp * kDenseCPB * (long long)A.stride;
+    for (int o = threadIdx.x * 16; o < nb; o += kDelBlock * 16) {
+        const long long go = g0 + o;
+        if (go + 16 <= total) {
+            *(uint4*)(stg + o) = *(const uint4*)(A.rx + go);
+        } else {
+            for (int b = 0; b < 16; ++b) stg[o + b] = (go + b < total) ? A.rx[go + b] : (uint8_t)0;
+        }
+    }
+}
+
+// pack_rows over the staged rows (LDS byte reads instead of global ones)
+__device__ __forceinline__ void pack_staged(const DelArgs& A, long long grp, const uint8_t* stg, uint32_t* rxb,
+                                            int lane) {
+    const int nch = (A.rw * 32 + 63) / 64;
+    for (int gg = threadIdx.x >> 6; gg < kDenseCPB; gg += kDelBlock / 64) {
+        long long cg = grp * kDenseCPB + gg;
+        cg = cg < A.B ? cg : A.B - 1;
+        const uint8_t* row = stg + gg * A.stride;  // (a padding row's bytes are zero; it stores nothing)
+        int ln = A.rx_len[cg];
+        ln = ln < 0 ? 0 : (ln > A.stride ? A.stride : ln);
+        for (int c0 = 0; c0 < nch; c0 += kPackU) {
+            uint32_t b[kPackU];
+#pragma unroll
+            for (int u = 0; u < kPackU; ++u) {
+                const int i = (c0 + u) * 64 + lane;
+                b[u] = i < ln ? (uint32_t)row[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kPackU; ++u) {
+                const unsigned long long msk = __ballot(b[u] == 1u);
+                const int wi = 2 * (c0 + u) + (lane & 1);
+                if (lane < 2 && wi < A.rw) rxb[gg * A.rw + wi] = (uint32_t)(msk >> (32 * lane));
+            }
+        }
+    }
+}
+
 // GT (n0 = 2): the table comes built (pcub_sc_deletion_build_table) and is copied into LDS, instead
 // of each workgroup building it: the build's registers (n02_table_entry) set the kernel's peak
 // (89 -> 79 VGPRs at 64 trellises: 6 waves a SIMD instead of 5)
@@ -151,7 +207,15 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
         const bool valid = cw < A.B;
         const long long c = valid ? cw : A.B - 1;  // padding codewords decode a duplicate, store nothing
         for (int i = threadIdx.x; i < CPB * WPC; i += kDelBlock) xs[i] = 0;
-        pack_rows<CPB>(A, grp, rxb, lane);  // received words bit-packed into LDS (sc_del_kern.h)
+        const int nb = (int)dense_stage_bytes(A.stride, A.rx);
+        if (nb) {  // received words: staged by 16-byte loads, then bit-packed from LDS
+            uint8_t* stg = (uint8_t*)(rxb + dense_stage_off(A.rw));
+            stage_rows(A, grp, stg, nb);
+            __syncthreads();
+            pack_staged(A, grp, stg, rxb, lane);
+        } else {
+            pack_rows<CPB>(A, grp, rxb, lane);  // received words bit-packed into LDS (sc_del_kern.h)
+        }
         __syncthreads();
 
         // segments (removeDeletionGuardBands' descent): trellis tr = jr * 2^TL + i is reached by

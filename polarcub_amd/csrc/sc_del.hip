@@ -32,8 +32,12 @@ std::atomic<int> g_dense{1};  // the table-driven layout allowed (pcub_sc_set_de
 // Status words of table-checked launches (one ring per device; sc_del_kern.h, DelArgs::gate): a
 // table-driven launch that rejects its table writes its launch id into its word, and the gated
 // fallback launch behind it on the same stream decodes the batch without the table only then.
-// Ids are unique per process, so a word left by an earlier launch never matches.
-constexpr int kGateRing = 1024;
+// Ids are unique per process, so a word left by an earlier launch never matches.  Limit: a word is
+// reused after kGateRing launches, so at most kGateRing table-checked launches may be in flight on
+// one device at once (streams included) -- one whose word was overwritten by a rejecting launch
+// 2^16 ids later would skip its fallback.  2^16 words (512 KiB a device) put that far beyond any
+// queue depth (round 5; 1,024 before).
+constexpr int kGateRing = 1 << 16;
 constexpr int kMaxDevices = 64;
 std::mutex g_gate_mu;
 unsigned long long* g_gate_ring[kMaxDevices] = {};

@@ -241,20 +241,46 @@ PCUB_HD QV<Q> q_shfl(const QV<Q>& v) {
     return w;
 }
 
+// The pair (a, b) = (the value of the pair's first lane, of its second) in both lanes of every
+// pair (lane, lane ^ H), H = 1 or 2 (inside a quad): two DPP broadcasts per 32 bits, quad_perm
+// [0,0,2,2] / [1,1,3,3] (H = 1) or [0,1,0,1] / [2,3,2,3] (H = 2), instead of an exchange with the
+// partner and a select of the q doubles by lane parity (round 5).  Wider pairs: the exchange.
+template <int Q, int H>
+PCUB_HD void q_pair(const QV<Q>& v, int lane, QV<Q>& a, QV<Q>& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (H == 1 || H == 2) {
+        constexpr int LO = H == 1 ? 0xA0 : 0x44, HI = H == 1 ? 0xF5 : 0xEE;
+#pragma unroll
+        for (int x = 0; x < Q; ++x) {
+            const unsigned long long bits = (unsigned long long)as_bits(v.p[x]);
+            const unsigned l0 = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)bits, LO, 0xF, 0xF, false);
+            const unsigned l1 = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(bits >> 32), LO, 0xF, 0xF, false);
+            const unsigned h0 = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)bits, HI, 0xF, 0xF, false);
+            const unsigned h1 = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(bits >> 32), HI, 0xF, 0xF, false);
+            a.p[x] = from_bits((long long)(((unsigned long long)l1 << 32) | l0));
+            b.p[x] = from_bits((long long)(((unsigned long long)h1 << 32) | h0));
+        }
+        return;
+    }
+#endif
+    const QV<Q> w = q_shfl<Q, H>(v);
+    const bool lo = (lane & H) == 0;
+#pragma unroll
+    for (int x = 0; x < Q; ++x) {
+        a.p[x] = lo ? v.p[x] : w.p[x];
+        b.p[x] = lo ? w.p[x] : v.p[x];
+    }
+}
+
 // A real node of M <= G positions, position (lane & (M-1)) in each lane; leaf u
 // indices UB .. UB+M-1 of the register subtree.  Returns this lane's symbol of
 // the node's re-encoding.
 template <int Q, int M>
 struct QXSub {
     static PCUB_HD int run(const QV<Q>& v, int ub, QInfo& qi, int lane) {
-        const QV<Q> w = q_shfl<Q, M / 2>(v);
         const bool lo = (lane & (M / 2)) == 0;
         QV<Q> a, b;
-#pragma unroll
-        for (int x = 0; x < Q; ++x) {
-            a.p[x] = lo ? v.p[x] : w.p[x];
-            b.p[x] = lo ? w.p[x] : v.p[x];
-        }
+        q_pair<Q, M / 2>(v, lane, a, b);
         int ym, yp;
         if constexpr (M == 2) {
             ym = 0;

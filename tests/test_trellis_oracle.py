@@ -126,8 +126,10 @@ def test_c_oracle_matches_reference():
         assert np.array_equal(info, c["info"]) and np.array_equal(xhat, c["xhat"])
 
 
+# (12, 4, 0), (13, 4, 0): main_deletion's own n0 = n // 3 at n = 12, 13 (256 and 512 trellises of
+# length 16), the shapes the GPU's n0 = 4 kernels are checked against the C oracle at
 @pytest.mark.parametrize("n,n0,ones", [(6, 2, 0), (8, 2, 0), (9, 3, 0), (10, 3, 0), (8, 2, 2), (7, 1, 0), (8, 4, 0),
-                                       (5, 5, 1)])
+                                       (5, 5, 1), (12, 4, 0), (13, 4, 0)])
 def test_c_oracle_matches_python_oracle(n, n0, ones):
     from oracle import orc
     rng = np.random.default_rng(10 * n + n0 + ones)
@@ -135,8 +137,9 @@ def test_c_oracle_matches_python_oracle(n, n0, ones):
     N = 1 << n
     frozen = (rng.random(N) < 0.5).astype(np.uint8)
     fval = (rng.random(N) < 0.5).astype(np.uint8)
+    nw = 5 if n < 12 else 2  # the Python restatement takes ~2 s a word at n = 13
     words = [tro.deletion_channel(tro.add_guard_bands([int(b) for b in rng.integers(0, 2, N)], n, n0, 0.1, ones), 0.1,
-                                  prng) for _ in range(5)]
+                                  prng) for _ in range(nw)]
     words += [[], [1], [0, 0, 1], [1] * (N + 3)]
     rx, ln = _padded(words)
     info, xhat = orc.decode_deletion(rx, ln, n, n0, 0.1, frozen, fval, ones)

@@ -2,7 +2,7 @@
 # Link A/B experiment kernels into the in-tree library without touching the library build.
 #   bash scripts/exp_build.sh <dir>
 # <dir>/inc<N>/ (or <dir>/inc/) holds experiment N's modified copies of csrc headers (searched before
-# csrc/), <dir>/kx*.hip the experiment
+# csrc/), <dir>/kx<N>.flags its extra compiler flags (optional), <dir>/kx*.hip the experiment
 # translation units: each defines its kernels in its own namespace (#define pcub pcubxN before including
 # sc_bin_kern.h) and an extern "C" pcub_exp_kernel_N(int v, int compact).  This script writes the
 # dispatcher pcub_exp_kernel(e, v, compact) -> pcub_exp_kernel_<e>, compiles everything for gfx950 and
@@ -28,7 +28,8 @@ N=$(ls $D/kx*.hip | wc -l)
 pids=()
 [ "${SKIP_COMPILE:-0}" = 1 ] || for f in $D/kx*.hip; do
   e=$(basename $f .hip); e=${e#kx}; INC=$D/inc$e; [ -d $INC ] || INC=$D/inc
-  /opt/rocm/bin/hipcc $FL -I$INC -I$R/include -I$CS -c $f -o ${f%.hip}.o &
+  XF=""; [ -f ${f%.hip}.flags ] && XF=$(cat ${f%.hip}.flags)  # extra compiler flags of experiment N
+  /opt/rocm/bin/hipcc $FL $XF -I$INC -I$R/include -I$CS -c $f -o ${f%.hip}.o &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done

@@ -9,9 +9,11 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 rc=$?; echo "smoke rc=$rc"; tail -1 $O/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 250 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-for t in c2 c4 c5; do
+for t in c2 c3 c4 c5 c5k64; do
   case $t in
     c2) A="--steps 10 --warmup 3";;
+    c3) A="--n 12 --steps 5 --warmup 2";;
+    c5k64) A="--workload deletion --del-k 64 --steps 10 --warmup 3";;
     c4) A="--workload qary --steps 10 --warmup 3";;
     c5) A="--workload deletion --steps 10 --warmup 3";;
   esac

@@ -33,6 +33,8 @@ extern "C" int pcub_sc_set_experiment(int e) {
     g_experiment = e;
     return old;
 }
+// the selected experiment, for the q-ary launcher's hook (sc_qary.hip)
+extern "C" int pcub_sc_experiment(void) { return g_experiment; }
 
 namespace {
 

@@ -100,26 +100,34 @@ PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, i
 }
 
 // Staged received words (round 5): a group's kDenseCPB rows are one contiguous run of CPB * stride
-// bytes (16-byte aligned when the batch is: CPB = 16), so the workgroup reads them with 16-byte
-// loads, every lane one or two, into an LDS staging area, and the waves bit-pack their rows from
-// there; pack_rows' byte loads cost a VMEM instruction and a ballot per 64 symbols of every row
-// (12 dependent-latency loads per C5 codeword).  The launcher sizes the LDS (dense_stage_bytes) and
-// the kernel stages whenever that size is nonzero.
+// bytes, so the workgroup reads them with 16-byte loads, every lane one or two, into an LDS staging
+// area, and the waves bit-pack their rows from there; pack_rows' byte loads cost a VMEM instruction
+// and a ballot per 64 symbols of every row (12 dependent-latency loads per C5 codeword).  Long rows
+// go in chunks of R rows (R a power of two, R * stride + 32 <= kDenseStageMax: n = 8 stages all 16
+// rows at once, n = 10 eight, n = 11 four), each chunk from the 16-byte boundary at or below its
+// first byte.  The launcher sizes the LDS (dense_stage_bytes) and the kernel stages whenever that
+// size is nonzero.
 constexpr int kDenseStageMax = 24 * 1024;  // staging bytes per workgroup, at most
 
+PCUB_HD int dense_stage_rows(int stride) {
+    int r = kDenseCPB;
+    while (r > 0 && (long long)r * stride + 32 > kDenseStageMax) r >>= 1;
+    return r;
+}
+
 PCUB_HD long long dense_stage_bytes(int stride, const void* rx) {
-    const long long b = (long long)kDenseCPB * stride;
-    return (b <= kDenseStageMax && ((unsigned long long)rx & 15ull) == 0) ? b : 0;
+    const int r = dense_stage_rows(stride);
+    return (r > 0 && ((unsigned long long)rx & 15ull) == 0) ? (long long)r * stride + 32 : 0;  // + the chunk's misalignment, + the last 16-byte load's tail
 }
 
 // the staging area: after the packed rows, 16-byte aligned
 PCUB_HD long long dense_stage_off(int rw) { return (((long long)kDenseCPB * rw + 3) / 4) * 4; }
 
-__device__ __forceinline__ void stage_rows(const DelArgs& A, long long grp, uint8_t* stg, int nb) {
+// bytes [a0, a0 + nb) of the batch's rows into stg (a0 16-byte aligned; bytes past the batch zero)
+__device__ __forceinline__ void stage_bytes(const DelArgs& A, long long a0, uint8_t* stg, int nb) {
     const long long total = A.B * (long long)A.stride;  // bytes of the batch's rows
-    const long long g0 = grp * kDenseCPB * (long long)A.stride;
     for (int o = threadIdx.x * 16; o < nb; o += kDelBlock * 16) {
-        const long long go = g0 + o;
+        const long long go = a0 + o;
         if (go + 16 <= total) {
             *(uint4*)(stg + o) = *(const uint4*)(A.rx + go);
         } else {
@@ -128,14 +136,14 @@ __device__ __forceinline__ void stage_rows(const DelArgs& A, long long grp, uint
     }
 }
 
-// pack_rows over the staged rows (LDS byte reads instead of global ones)
-__device__ __forceinline__ void pack_staged(const DelArgs& A, long long grp, const uint8_t* stg, uint32_t* rxb,
-                                            int lane) {
+// pack_rows over staged rows r0 .. r0 + R - 1 of the group (row r0 at stg0; LDS byte reads)
+__device__ __forceinline__ void pack_staged(const DelArgs& A, long long grp, const uint8_t* stg0, int r0, int R,
+                                            uint32_t* rxb, int lane) {
     const int nch = (A.rw * 32 + 63) / 64;
-    for (int gg = threadIdx.x >> 6; gg < kDenseCPB; gg += kDelBlock / 64) {
+    for (int gg = r0 + (threadIdx.x >> 6); gg < r0 + R; gg += kDelBlock / 64) {
         long long cg = grp * kDenseCPB + gg;
         cg = cg < A.B ? cg : A.B - 1;
-        const uint8_t* row = stg + gg * A.stride;  // (a padding row's bytes are zero; it stores nothing)
+        const uint8_t* row = stg0 + (gg - r0) * A.stride;  // (a padding row's bytes are zero; it stores nothing)
         int ln = A.rx_len[cg];
         ln = ln < 0 ? 0 : (ln > A.stride ? A.stride : ln);
         for (int c0 = 0; c0 < nch; c0 += kPackU) {
@@ -207,12 +215,18 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
         const bool valid = cw < A.B;
         const long long c = valid ? cw : A.B - 1;  // padding codewords decode a duplicate, store nothing
         for (int i = threadIdx.x; i < CPB * WPC; i += kDelBlock) xs[i] = 0;
-        const int nb = (int)dense_stage_bytes(A.stride, A.rx);
-        if (nb) {  // received words: staged by 16-byte loads, then bit-packed from LDS
+        if (dense_stage_bytes(A.stride, A.rx)) {  // received words: staged by 16-byte loads, packed from LDS
             uint8_t* stg = (uint8_t*)(rxb + dense_stage_off(A.rw));
-            stage_rows(A, grp, stg, nb);
-            __syncthreads();
-            pack_staged(A, grp, stg, rxb, lane);
+            const int R = dense_stage_rows(A.stride);
+            for (int r0 = 0; r0 < CPB; r0 += R) {
+                const long long b0 = (grp * CPB + r0) * (long long)A.stride;
+                const long long a0 = b0 & ~15ll;
+                const int mis = (int)(b0 - a0);
+                if (r0) __syncthreads();  // the previous chunk's rows are packed
+                stage_bytes(A, a0, stg, R * A.stride + mis);
+                __syncthreads();
+                pack_staged(A, grp, stg + mis, r0, R, rxb, lane);
+            }
         } else {
             pack_rows<CPB>(A, grp, rxb, lane);  // received words bit-packed into LDS (sc_del_kern.h)
         }

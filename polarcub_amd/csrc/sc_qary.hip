@@ -68,6 +68,11 @@ __global__ __launch_bounds__(kQBlock) void k_encode_qary(const uint8_t* info, lo
     }
 }
 
+// A/B experiments (sc_bin.hip's hook, scripts/exp_build.sh): a candidate split-level tiled-root
+// kernel linked in as pcub_exp_qkernel, launched while pcub_sc_set_experiment selects it
+extern "C" __attribute__((weak)) void* pcub_exp_qkernel(int e, int q, int S, int G);
+extern "C" int pcub_sc_experiment(void);
+
 int g_qlanes = 4;  // requested lanes per codeword (pcub_sc_set_qary_lanes)
 int g_qylds = 1;   // symbols in LDS where a twin kernel exists and fits (pcub_sc_set_qary_lds)
 constexpr size_t kQLdsPerCu = 160 * 1024;
@@ -216,7 +221,9 @@ int decode_qary_impl(const double* xy, int64_t B, int32_t log2N, int32_t q, int3
     A.ysym = c.yl ? nullptr : (uint32_t*)(slots + (size_t)A.nslots * (N / c.G - 2 * c.sr()) * ((q + 1) / 2) * sizeof(double2));
     // rows in the wave's own tiles: the uniform-base twin where one is instantiated
     QKern kern = nullptr;
-    if (g_qtr && c.hl && tile == 64 / c.G) kern = qary_kernel_h_tr(q, c.S, c.G);
+    if (pcub_exp_qkernel && pcub_sc_experiment() && c.hl && tile == 64 / c.G)
+        kern = (QKern)pcub_exp_qkernel(pcub_sc_experiment(), q, c.S, c.G);
+    if (!kern && g_qtr && c.hl && tile == 64 / c.G) kern = qary_kernel_h_tr(q, c.S, c.G);
     if (!kern) kern = qkernel(q, log2N);
     hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(kQBlock), qlaunch_lds(q, log2N), st, A);
     return (int)hipGetLastError();

@@ -265,3 +265,35 @@ def test_dense_layout_matches_lane_layout(sc, n0, n):
     for i in list(range(0, len(words), 9)) + [len(words) - 3, len(words) - 1]:
         x_ref, i_ref = tro.decode_deletion(words[i], n, n0, pd, frozen, fval)
         assert list(outs[0][0][i]) == i_ref and list(outs[0][1][i]) == x_ref, i
+
+
+@pytest.mark.parametrize("n0,n", [(2, 8), (2, 10), (3, 10), (3, 11)])
+def test_dense_staging_any_stride(sc, n0, n):
+    """The table-driven kernel stages its group's received rows into LDS in chunks of R rows, each
+    from the 16-byte boundary below its first byte (sc_del_dense.h): widening the rows by zero
+    columns (strides that move every chunk's start off the boundary, and R with them) and a batch
+    base off 16 bytes (no staging: pack_rows) decode identically."""
+    N = 1 << n
+    rng = np.random.default_rng(11 * n + n0)
+    prng = random.Random(5 * n + n0)
+    frozen = (rng.random(N) < 0.55).astype(np.uint8)
+    frozen[: N // 8] = 1
+    fval = np.zeros(N, np.uint8)
+    words = [tro.deletion_channel(tro.add_guard_bands([int(b) for b in rng.integers(0, 2, N)], n, n0, 0.1, 0), 0.1, prng)
+             for _ in range(45)]
+    rxt, ln = sc.pad_words(words)
+    d = sc.DeletionDecoder(sc.CodeSpec(N, frozen, fval, device="cuda"), n0, 0.1)
+    assert d.dense_layout(rxt.shape[1], rxt.device)
+    ref = [t.cpu().numpy() for t in d.decode(rxt, ln)]
+    for extra in (1, 5, 13, 16 * 16 + 3):
+        wide = torch.cat([rxt, torch.zeros(rxt.shape[0], extra, dtype=rxt.dtype, device=rxt.device)], 1).contiguous()
+        out = [t.cpu().numpy() for t in d.decode(wide, ln)]
+        assert np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1]), extra
+    buf = torch.zeros(rxt.numel() + 16, dtype=rxt.dtype, device=rxt.device)
+    off = buf[3: 3 + rxt.numel()].view(rxt.shape)
+    off.copy_(rxt)
+    out = [t.cpu().numpy() for t in d.decode(off, ln)]
+    assert np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1])
+    for i in (0, 22, 44):
+        x_ref, i_ref = tro.decode_deletion(words[i], n, n0, 0.1, frozen, fval)
+        assert list(ref[0][i]) == i_ref and list(ref[1][i]) == x_ref, i

@@ -197,11 +197,118 @@ struct XSub {
     }
 };
 
+// Rate-1 nodes (round 5).  In a node with no frozen position, SC's decisions are the hard decisions
+// of its inputs whenever every minus transform inside it keeps the orientation its inputs give it:
+// with t = (1 - r) / (1 + r) per value, a minus output has t = t_a t_b (exactly, before rounding) and
+// a plus output under the hard decision of its left sibling t >= max(t_a, t_b), so every value in the
+// node has t >= prod t_i over the node's inputs.  When that product is >= 2^-17 every canonical
+// minus transform compares p0 = 1 + ra rb against p1 = ra + rb with p0 - p1 = (1 - ra)(1 - rb) >=
+// 2^-17, far above the 2^-51 its roundings can move, so p1 > p0 never holds, every output ratio is
+// < 1 and carries the XOR of its inputs' orientations, every plus transform takes the same-orientation
+// branch, and every leaf decides its value's orientation: the node's re-encoding is the inputs' signs
+// and its decisions are their polar transform (an involution) -- the values the recursion would compute
+// bit for bit.  A NaN ((0, 0)) or a tie (r = 1) makes the product NaN or 0 and fails the test.  The
+// test runs per codeword (its G lanes) and the wave takes the shortcut only when all its codewords
+// pass (a uniform branch); otherwise the recursion runs as before.
+template <int G>
+PCUB_HD uint64_t spread_stride(uint64_t x) {  // bit t -> bit t * G (the inverse of gather_stride)
+    if constexpr (G == 1) {
+        return x;
+    } else if constexpr (G == 2) {
+        x &= 0xFFFFFFFFull;
+        x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+        x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+        x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+        x = (x | (x << 2)) & 0x3333333333333333ull;
+        return (x | (x << 1)) & 0x5555555555555555ull;
+    } else if constexpr (G == 4) {
+        x &= 0xFFFFull;
+        x = (x | (x << 24)) & 0x000000FF000000FFull;
+        x = (x | (x << 12)) & 0x000F000F000F000Full;
+        x = (x | (x << 6)) & 0x0303030303030303ull;
+        return (x | (x << 3)) & 0x1111111111111111ull;
+    } else if constexpr (G == 8) {
+        x &= 0xFFull;
+        x = (x | (x << 28)) & 0x0000000F0000000Full;
+        x = (x | (x << 14)) & 0x0003000300030003ull;
+        return (x | (x << 7)) & 0x0101010101010101ull;
+    } else if constexpr (G == 16) {
+        x &= 0xFull;
+        x = (x | (x << 30)) & 0x0000000300000003ull;
+        return (x | (x << 15)) & 0x0001000100010001ull;
+    } else if constexpr (G == 32) {
+        return ((x & 1ull) | ((x & 2ull) << 31));
+    } else {
+        static_assert(G == 64, "lanes per codeword");
+        return x & 1ull;
+    }
+}
+
+// x OR-ed over the aligned group of G lanes
+template <int G, int M = 1>
+PCUB_HD uint64_t or_group(uint64_t x) {
+    if constexpr (M >= G) {
+        return x;
+    } else {
+        return or_group<G, 2 * M>(x | (uint64_t)as_bits(xor_shfl_c<M>(from_bits((long long)x))));
+    }
+}
+
+template <int G, int M = 1>
+PCUB_HD double mul_group(double x) {
+    if constexpr (M >= G) {
+        return x;
+    } else {
+        return mul_group<G, 2 * M>(x * xor_shfl_c<M>(x));
+    }
+}
+
+// every codeword of the wave passes the rate-1 test on its L values per lane (a wave-uniform answer)
+template <int L, int G>
+PCUB_HD bool rate1_sure(const double* v) {
+    double p1 = 1.0, p2 = 1.0;  // prod (1 - r), prod (1 + r) over the codeword's values
+#pragma unroll
+    for (int t = 0; t < L; ++t) {
+        const double r = __builtin_fabs(v[t]);
+        p1 *= 1.0 - r;
+        p2 *= 1.0 + r;
+    }
+    p1 = mul_group<G>(p1);
+    p2 = mul_group<G>(p2);
+    const bool ok = p1 >= 0x1p-17 * p2;  // false on NaN
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ballot_w64(!ok) == 0ull;
+#else
+    return ok;
+#endif
+}
+
+// the rate-1 node of L values per lane at virtual leaf BASE_V: local encoding bits = the values'
+// orientations; decisions u_{BASE_V*G ..} = the polar transform of the node's natural-order encoding
+// (position t*G + j is lane j's local bit t)
+template <int L, int BASE_V, int G>
+PCUB_HD uint32_t rate1_node(const double* v, uint64_t& ub, int lane) {
+    static_assert(L * G <= 64, "one window");
+    uint32_t h = 0;
+#pragma unroll
+    for (int t = 0; t < L; ++t) h |= (hi32(v[t]) >> 31) << t;
+    const uint64_t x = or_group<G>(spread_stride<G>(h) << (lane & (G - 1)));
+    ub |= polar_bits(x) << (BASE_V * G);
+    return h;
+}
+
 // Register-resident virtual subtree of L values per lane; virtual leaf BASE_V
 // covers real u positions [BASE_V*G, BASE_V*G + G).  Returns L local encoding bits.
 template <int L, int BASE_V, int G>
 struct SubV {
     static PCUB_HD uint32_t run(const double* v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane) {
+        // (not in the deletion kernels' 16-lane subtrees: their rows hold ties and (0, 0) pairs, and
+        // there the test cost more than it saved -- C5 853 -> 820 M cw/s, K = 64 305 -> 298 M)
+        if constexpr (L >= 2 && L * G >= 16 && G <= 8) {
+            // a rate-1 node (no frozen position; wave-uniform) whose codewords all pass the test
+            constexpr uint64_t NM = (L * G == 64) ? ~0ull : ((1ull << (L * G)) - 1ull);
+            if (((fm >> (BASE_V * G)) & NM) == 0ull && rate1_sure<L, G>(v)) return rate1_node<L, BASE_V, G>(v, ub, lane);
+        }
         if constexpr (L == 1) {
             static_assert(G >= 2, "G == 1 stops at L == 2");
             return XSub<G, BASE_V * G>::run(v[0], ub, fm, fv, lane);

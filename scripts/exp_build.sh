@@ -6,8 +6,8 @@
 # translation units: each defines its kernels in its own namespace (#define pcub pcubxN before including
 # sc_bin_kern.h) and an extern "C" pcub_exp_kernel_N(int v, int compact).  This script writes the
 # dispatcher pcub_exp_kernel(e, v, compact) -> pcub_exp_kernel_<e>, compiles everything for gfx950 and
-# relinks polarcub_amd/lib/libpolarcub_hip.so from the library's objects plus these (the library's stamp
-# is left alone, so the next `python -m polarcub_amd.build` relinks the clean library).
+# relinks polarcub_amd/lib/libpolarcub_hip.so from the library's objects plus these, and removes the
+# library's stamp so that the next `python -m polarcub_amd.build` relinks the clean library.
 set -eu
 D=$(cd "$1" && pwd)
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -42,5 +42,7 @@ from polarcub_amd import build as b
 objs = [b._obj(s) for s in b.SOURCES] + sorted(glob.glob(os.path.join(D, "kx*.o"))) + [os.path.join(D, "dispatch.o")]
 subprocess.run([b.HIPCC, "--offload-arch=" + b.ARCH, "-shared", "-fPIC"] + objs + ["-o", b.LIB + ".tmp"], check=True)
 os.replace(b.LIB + ".tmp", b.LIB)
+if os.path.exists(b.LIB + ".sha256"):
+    os.remove(b.LIB + ".sha256")  # the next library build relinks without the experiments
 print("linked", len(objs), "objects")
 PY

@@ -92,6 +92,41 @@ def test_rate0_blocks(sc, variant):
     sc.set_variant()
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_rate1_blocks(sc, variant):
+    """Frozen sets with large aligned all-information (rate-1) blocks, decoded through the rate-1
+    shortcut (sc_bin_body.h: hard decisions when every codeword of the wave passes the reliability
+    test) and through the recursion when one does not: per-codeword reliabilities from near-certain
+    to noise, exact ties, near ties and (0, 0) rows in the same waves, bit-exact against the oracle."""
+    from oracle import orc
+    sc.set_variant(variant)
+    rng = np.random.default_rng(19 + variant)
+    for n, B in [(6, 300), (8, 700), (10, 900), (12, 160)]:
+        N = 1 << n
+        frozen = (rng.random(N) < 0.5).astype(np.uint8)
+        w = N // 4
+        while w >= 16:
+            for _ in range(2):
+                s = int(rng.integers(N // (2 * w), N // w)) * w
+                frozen[s:s + w] = 0
+            w //= 2
+        frozen[: N // 8] = 1
+        fval = (rng.random(N) < 0.5).astype(np.uint8)
+        mu = rng.choice([1.0, 6.0, 20.0, 60.0], size=(B, 1), p=[0.1, 0.3, 0.3, 0.3])
+        llr = rng.normal(mu, 2.0, (B, N)) * np.where(rng.random((B, N)) < 0.5, 1, -1)
+        llr[rng.random((B, N)) < 0.002] = 0.0      # exact ties
+        llr[rng.random((B, N)) < 0.002] = 1e-13    # near ties
+        p1 = 1.0 / (1.0 + np.exp(llr))
+        xy = np.stack([1.0 - p1, p1], axis=-1)
+        xy[rng.random((B, N)) < 0.001] = 0.0       # (0, 0) rows
+        code = sc.CodeSpec(N, frozen, fval)
+        info, xhat = sc.BinaryDecoder(code).decode(torch.from_numpy(xy).cuda())
+        ri, rx = orc.decode_bin(xy, frozen, fval)
+        assert np.array_equal(info.cpu().numpy(), ri), (n, B)
+        assert np.array_equal(xhat.cpu().numpy(), rx), (n, B)
+    sc.set_variant()
+
+
 @pytest.mark.parametrize("n", [1, 3, 5, 8, 10])
 def test_encode_matches_reference(sc, n):
     g = load_golden("encode_binary")

@@ -270,7 +270,7 @@ PCUB_HD bool rate1_sure(const double* v) {
 #pragma unroll
     for (int t = 0; t < L; ++t) {
         const double r = __builtin_fabs(v[t]);
-        p1 *= 1.0 - r;
+        p1 *= __builtin_fmax(1.0 - r, 0.0);  // r > 1 (only from negative root rows) or NaN: 0, fails
         p2 *= 1.0 + r;
     }
     p1 = mul_group<G>(p1);

@@ -176,3 +176,17 @@ def test_wide_shapes_vs_oracle(n0, n, ones, implicit_base):
     for i, w in enumerate(words):
         xr, ir = tro.decode_deletion(w, n, n0, pd, frozen, fval, ones=ones)
         assert list(info[i]) == ir and list(xhat[i]) == xr, i
+
+
+def test_dense_trellis_matches_trel():
+    """trellis_dense.h (the dense-slot trellises of the n0 >= 3 decode path, no guard-band ones)
+    against trellis_body.h's Trel on random segments (n0 = 3 and 4, pd from 0 to 1, lengths around,
+    below and above the trellis length) and random decision histories: every stage holds the same
+    edges in the same creation order, the same vertices in the same insertion order, bit-identical
+    probabilities and collapsed values (tests/emu/dtrel_check.cpp)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "emu")], check=True)
+    exe = os.path.join(ROOT, "tests", "emu", "build", "dtrel_check")
+    for seed in (11, 12):
+        r = subprocess.run([exe, "100000", str(seed)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert " 0 mismatches" in r.stdout

@@ -246,6 +246,8 @@ class Deletion:
             self.construction = "Bhattacharyya ranking stand-in, K=%d" % K
         self.code = sc.CodeSpec.from_frozen_set(self.N, frozen, 200, device=device)
         self.K = self.code.K
+        if a.del_lanes:
+            sc.set_deletion_lanes(a.del_lanes)
         self.dec = sc.DeletionDecoder(self.code, self.n0, self.pd, self.ones)
         # Philox keyed by the global codeword index: rank r's shard is codewords [r*B, (r+1)*B) of
         # the one-GPU run, so sharded counters sum to the single run's
@@ -554,6 +556,7 @@ def build_parser():
     ap.add_argument("--n0", type=int, default=None, help="deletion: log2 inputs per trellis (default n // 3)")
     ap.add_argument("--ones", type=int, default=0, help="deletion: guard-band ones (numberOfOnesToAddAtBothEndsOfGuardbands)")
     ap.add_argument("--del-k", type=int, default=0, help="deletion: information bits (0 = the configuration's frozen set)")
+    ap.add_argument("--del-lanes", type=int, default=0, help="deletion: lanes a codeword of the table-driven layout (0 = the library's)")
     ap.add_argument("--pd", type=float, default=0.1, help="deletion probability")
     ap.add_argument("--xi", type=float, default=0.1, help="guard-band parameter")
     ap.add_argument("--q", type=int, default=4)

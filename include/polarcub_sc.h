@@ -162,6 +162,9 @@ int64_t pcub_sc_deletion_table_bytes(int32_t n0);
 /* Diagnostics: allow (1, the default) or forbid (0) the table-driven layout, 16 lanes per codeword
  * (DESIGN 3.2); returns the previous setting.  Decisions are identical either way. */
 int pcub_sc_set_deletion_dense(int32_t on);
+/* Tuning hook: lanes a codeword of that layout, 8 (default) or 16, or 4 (up to 64 trellises; 8
+ * beyond); returns the previous value, -1 for another value.  Decisions are identical either way. */
+int pcub_sc_set_deletion_lanes(int32_t lanes);
 /* 1 when pcub_sc_decode_deletion_tab would run the table-driven layout for this shape, received
  * row stride, table and pd (diagnostics: which kernel a profile names). */
 int pcub_sc_deletion_dense_layout(int32_t n, int32_t n0, int32_t ones, int32_t stride, const double* table, double pd);

@@ -95,6 +95,8 @@ def lib():
     L.pcub_sc_deletion_table_bytes.argtypes = [_i32]
     L.pcub_sc_set_deletion_dense.restype = ctypes.c_int
     L.pcub_sc_set_deletion_dense.argtypes = [_i32]
+    L.pcub_sc_set_deletion_lanes.restype = ctypes.c_int
+    L.pcub_sc_set_deletion_lanes.argtypes = [_i32]
     L.pcub_sc_deletion_dense_layout.restype = ctypes.c_int
     L.pcub_sc_deletion_dense_layout.argtypes = [_i32, _i32, _i32, _i32, _c_void_p, ctypes.c_double]
     L.pcub_sc_deletion_build_table.restype = ctypes.c_int
@@ -201,7 +203,7 @@ EXPORTS = ["pcub_abi_version", "pcub_sc_decode_bin_workspace", "pcub_sc_decode_b
            "pcub_sc_decode_bin_compact", "pcub_mc_info_qary", "pcub_mc_channel_qsc", "pcub_mc_deletion",
            "pcub_mc_run_bin_workspace", "pcub_mc_run_bin", "pcub_sc_deletion_table_bytes",
            "pcub_sc_deletion_build_table", "pcub_sc_decode_deletion_tab", "pcub_sc_leaf_deletion_tab",
-           "pcub_sc_set_deletion_dense", "pcub_sc_deletion_dense_layout", "pcub_sc_bin_tile", "pcub_sc_decode_bin_tiled",
+           "pcub_sc_set_deletion_dense", "pcub_sc_set_deletion_lanes", "pcub_sc_deletion_dense_layout", "pcub_sc_bin_tile", "pcub_sc_decode_bin_tiled",
            "pcub_sc_decode_bin_compact_tiled", "pcub_mc_channel_tiled", "pcub_mc_channel_norm_tiled",
            "pcub_mc_channel_qsc_tiled", "pcub_sc_qary_tile", "pcub_sc_decode_qary_tiled",
            "pcub_mc_run_qary_workspace", "pcub_mc_run_qary", "pcub_mc_run_deletion_workspace", "pcub_mc_run_deletion"]

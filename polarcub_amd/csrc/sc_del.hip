@@ -28,6 +28,7 @@ constexpr int kMaxOnes = 3;
 constexpr int kMaxStride = 1 << 24;
 
 std::atomic<int> g_dense{1};  // the table-driven layout allowed (pcub_sc_set_deletion_dense)
+std::atomic<int> g_dense_lanes{8};  // lanes a codeword of the table-driven layout (8, 16; 4 up to 64 trellises)
 
 // Status words of table-checked launches (one ring per device; sc_del_kern.h, DelArgs::gate): a
 // table-driven launch that rejects its table writes its launch id into its word, and the gated
@@ -127,10 +128,17 @@ OnesProbs ones_probs(int ones, double pd) {
 // the table-driven layout (sc_del_dense.h) when the stage has a table: n0 = 2 (the caller's, or
 // built per workgroup) or n0 = 3 with a table given (checked on the device: tab_ok), no ones,
 // 16 .. 256 trellises, and the group's received words fit LDS bit-packed
+// lanes a codeword of the table-driven layout for 2^tb trellises (pcub_sc_set_deletion_lanes)
+int dense_lanes(int tb) {
+    const int g = g_dense_lanes.load(std::memory_order_relaxed);
+    return (tb <= 6 || g != 4) ? g : 8;  // 4 lanes only up to 64 trellises
+}
+
 bool use_dense(int n, int n0, int ones, int stride, const double* table) {
     const long long rw = ((long long)stride + 31) / 32;
+    const long long cpb = kDelBlock / dense_lanes(n - n0);
     return g_dense.load(std::memory_order_relaxed) && ones == 0 && (n0 == 2 || (n0 == 3 && table)) &&
-           n - n0 >= 4 && (long long)kDenseCPB * rw * 4 <= kDenseMaxRxLds && del_kernel_dense(n0, n - n0) != nullptr;
+           n - n0 >= 4 && cpb * rw * 4 <= kDenseMaxRxLds && del_kernel_dense(n0, n - n0, false, dense_lanes(n - n0)) != nullptr;
 }
 
 // A persistent grid for kernel k: one resident grid striding over the codeword groups.  The occupancy
@@ -186,17 +194,19 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
         const int rc = gate_slot(&A.gate, &A.gate_id);
         if (rc) return rc;
     }
-    DelKern k = dense ? del_kernel_dense(n0, n - n0, n0 == 2 && A.tab) : kern;
+    const int dg = dense_lanes(n - n0);
+    DelKern k = dense ? del_kernel_dense(n0, n - n0, n0 == 2 && A.tab, dg) : kern;
     // the general kernel's workgroup: 256 threads, or T for 512 / 1024 trellises (one codeword)
     const int blk = dense ? kDelBlock : ((n - n0) > 8 ? 1 << (n - n0) : kDelBlock);
-    long long cpb = dense ? kDenseCPB : blk >> (n - n0);
+    long long cpb = dense ? kDelBlock / dg : blk >> (n - n0);
     long long grid = (B + cpb - 1) / cpb;
     // bit-packed received words in LDS when the group's words fit in 32 KiB (always for
     // the 64-trellis shapes; very long padded rows of small codes parse from HBM)
     A.rw = (dense || cpb * rw * 4 <= 32768) ? (int)rw : 0;
     size_t lds = A.rw ? (size_t)(cpb * rw * 4) : 0;
     // the table-driven kernel's staging area for its group's raw rows (sc_del_dense.h)
-    if (dense && dense_stage_bytes(stride, rx)) lds = (size_t)(dense_stage_off((int)rw) * 4 + dense_stage_bytes(stride, rx));
+    if (dense && dense_stage_bytes(stride, rx, (int)cpb))
+        lds = (size_t)(dense_stage_off((int)rw, (int)cpb) * 4 + dense_stage_bytes(stride, rx, (int)cpb));
     // n0 = 2 without ones (and the table-driven layout): each workgroup first builds or copies the
     // segment-state table, so the launch is persistent
     if (dense || (n0 == 2 && ones == 0)) grid = resident_grid(k, lds, grid);
@@ -209,12 +219,12 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     DelArgs F = A;
     F.tab = nullptr;
     const bool fb_dense = n0 == 2;
-    const DelKern fk = fb_dense ? del_kernel_dense(2, n - n0, false) : kern;
-    const long long fcpb = fb_dense ? kDenseCPB : kDelBlock >> (n - n0);
+    const DelKern fk = fb_dense ? del_kernel_dense(2, n - n0, false, dg) : kern;
+    const long long fcpb = fb_dense ? kDelBlock / dg : kDelBlock >> (n - n0);
     F.rw = (fb_dense || fcpb * rw * 4 <= 32768) ? (int)rw : 0;
     size_t flds = F.rw ? (size_t)(fcpb * rw * 4) : 0;
-    if (fb_dense && dense_stage_bytes(stride, rx))
-        flds = (size_t)(dense_stage_off((int)rw) * 4 + dense_stage_bytes(stride, rx));
+    if (fb_dense && dense_stage_bytes(stride, rx, (int)fcpb))
+        flds = (size_t)(dense_stage_off((int)rw, (int)fcpb) * 4 + dense_stage_bytes(stride, rx, (int)fcpb));
     const long long fgrid = resident_grid(fk, flds, (B + fcpb - 1) / fcpb);
     hipLaunchKernelGGL(fk, dim3((unsigned)fgrid), dim3(kDelBlock), flds, (hipStream_t)stream, F);
     return (int)hipGetLastError();
@@ -263,6 +273,13 @@ extern "C" int pcub_sc_leaf_deletion_tab(const uint8_t* rx, const int32_t* rx_le
                                          void* stream) {
     return launch_del(true, rx, rx_len, B, stride, n, n0, ones, pd, frozen_mask, frozen_val, frozen_val_cw, K,
                       info_words, xhat_words, leaf, table, stream);
+}
+
+// Tuning hook (not part of the stable ABI): lanes a codeword of the table-driven deletion layout,
+// 8 (the default), 16, or 4 (up to 64 trellises; 8 beyond); returns the previous value, or -1.
+extern "C" int pcub_sc_set_deletion_lanes(int32_t g) {
+    if (g != 4 && g != 8 && g != 16) return -1;
+    return g_dense_lanes.exchange(g);
 }
 
 extern "C" int pcub_sc_set_deletion_dense(int32_t on) {

@@ -5,10 +5,11 @@
 // costs one table load per subtree input, so the trellis stages no longer need a lane each:
 // k_sc_del's layout (one lane per trellis, the memoryless subtree decoded by 16 lanes of wave 0
 // after an LDS exchange and two barriers) leaves three waves of four idle in every subtree call.
-// Here a codeword owns G = 16 lanes of one wave for the whole decode (four codewords a wave,
-// sixteen a workgroup): lane j holds the LV = T / 16 trellises at memoryless positions
-// p = j + 16 t, looks their values up, and decodes the subtree in registers with the binary
-// kernel's WinTree / DelWin.  No LDS exchange and no barrier inside the walk.
+// Here a codeword owns G lanes of one wave for the whole decode (G = 8 by default: eight codewords a
+// wave, thirty-two a workgroup; 16 and, up to 64 trellises, 4 through pcub_sc_set_deletion_lanes):
+// lane j holds the LV = T / G trellises at memoryless positions p = j + G t, looks their values
+// up, and decodes the subtree in registers with the binary kernel's WinTree (DelWin at G = 16).
+// No LDS exchange and no barrier inside the walk.
 //
 // Same decisions as k_sc_del (and the reference): the values are the table's, which are the
 // per-lane values bit for bit (tests/emu/del_emu.cpp checks every one), the subtree is the same
@@ -20,8 +21,8 @@
 
 namespace pcub {
 
-constexpr int kDenseG = 16;                     // lanes per codeword
-constexpr int kDenseCPB = kDelBlock / kDenseG;  // codewords per workgroup
+constexpr int kDenseG = 16;                     // lanes per codeword of the 16-lane form (DelWin's windows)
+constexpr int kDenseCPB = kDelBlock / kDenseG;  // its codewords per workgroup (the staging helpers' default)
 constexpr int kDenseMaxRxLds = 48 * 1024;       // bit-packed received words per workgroup, at most
 
 // slot of subtree input k (history hist: bit i = the i-th returned bit) in a state's row
@@ -66,16 +67,16 @@ PCUB_HD uint32_t packed_bits(const uint32_t* w, int s, int m, int rw) {
     return (uint32_t)(x >> sh) & ((1u << m) - 1u);
 }
 
-// The segments of the 2^(TB-4) trellises tr = jr * 2^(TB-4) + i of one lane (removeDeletionGuardBands'
-// descent, segment_of_packed): the 4 halvings of jr, shared by them, then a split per level, each
+// The segments of the 2^(TB-GB) trellises tr = jr * 2^(TB-GB) + i of one lane (removeDeletionGuardBands'
+// descent, segment_of_packed): the GB halvings of jr (G = 2^GB lanes a codeword), shared by them, then a split per level, each
 // range halved and both halves trimmed; entry i = [sa[i], se[i]).
-template <int TB>
+template <int TB, int GB = 4>
 PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, int* se) {
-    constexpr int TL = TB - 4;
+    constexpr int TL = TB - GB;
     int a = 0, e = len;
     trim_range_packed(pw, a, e);
 #pragma unroll
-    for (int k = 3; k >= 0; --k) {
+    for (int k = GB - 1; k >= 0; --k) {
         const int h = (e - a) / 2;
         if ((jr >> k) & 1u) a += h;
         else e = a + h;
@@ -99,29 +100,29 @@ PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, i
     }
 }
 
-// Staged received words (round 5): a group's kDenseCPB rows are one contiguous run of CPB * stride
-// bytes, so the workgroup reads them with 16-byte loads, every lane one or two, into an LDS staging
-// area, and the waves bit-pack their rows from there; pack_rows' byte loads cost a VMEM instruction
+// Staged received words (round 5): a group's CPB rows are one contiguous run of CPB * stride
+// bytes, so the workgroup reads them with 16-byte loads, a few a lane, into an LDS staging area,
+// and the waves bit-pack their rows from there; pack_rows' byte loads cost a VMEM instruction
 // and a ballot per 64 symbols of every row (12 dependent-latency loads per C5 codeword).  Long rows
-// go in chunks of R rows (R a power of two, R * stride + 32 <= kDenseStageMax: n = 8 stages all 16
-// rows at once, n = 10 eight, n = 11 four), each chunk from the 16-byte boundary at or below its
-// first byte.  The launcher sizes the LDS (dense_stage_bytes) and the kernel stages whenever that
+// go in chunks of R rows (R a power of two, R * stride + 32 <= kDenseStageMax: at 8 lanes a codeword
+// n = 8 stages all 32 rows at once, n = 10 four, n = 11 two), each chunk from the 16-byte boundary
+// at or below its first byte.  The launcher sizes the LDS (dense_stage_bytes) and the kernel stages whenever that
 // size is nonzero.
 constexpr int kDenseStageMax = 24 * 1024;  // staging bytes per workgroup, at most
 
-PCUB_HD int dense_stage_rows(int stride) {
-    int r = kDenseCPB;
+PCUB_HD int dense_stage_rows(int stride, int cpb = kDenseCPB) {
+    int r = cpb;
     while (r > 0 && (long long)r * stride + 32 > kDenseStageMax) r >>= 1;
     return r;
 }
 
-PCUB_HD long long dense_stage_bytes(int stride, const void* rx) {
-    const int r = dense_stage_rows(stride);
+PCUB_HD long long dense_stage_bytes(int stride, const void* rx, int cpb = kDenseCPB) {
+    const int r = dense_stage_rows(stride, cpb);
     return (r > 0 && ((unsigned long long)rx & 15ull) == 0) ? (long long)r * stride + 32 : 0;  // + the chunk's misalignment, + the last 16-byte load's tail
 }
 
 // the staging area: after the packed rows, 16-byte aligned
-PCUB_HD long long dense_stage_off(int rw) { return (((long long)kDenseCPB * rw + 3) / 4) * 4; }
+PCUB_HD long long dense_stage_off(int rw, int cpb = kDenseCPB) { return (((long long)cpb * rw + 3) / 4) * 4; }
 
 // bytes [a0, a0 + nb) of the batch's rows into stg (a0 16-byte aligned; bytes past the batch zero)
 __device__ __forceinline__ void stage_bytes(const DelArgs& A, long long a0, uint8_t* stg, int nb) {
@@ -137,11 +138,12 @@ __device__ __forceinline__ void stage_bytes(const DelArgs& A, long long a0, uint
 }
 
 // pack_rows over staged rows r0 .. r0 + R - 1 of the group (row r0 at stg0; LDS byte reads)
+template <int CPB>
 __device__ __forceinline__ void pack_staged(const DelArgs& A, long long grp, const uint8_t* stg0, int r0, int R,
                                             uint32_t* rxb, int lane) {
     const int nch = (A.rw * 32 + 63) / 64;
     for (int gg = r0 + (threadIdx.x >> 6); gg < r0 + R; gg += kDelBlock / 64) {
-        long long cg = grp * kDenseCPB + gg;
+        long long cg = grp * CPB + gg;
         cg = cg < A.B ? cg : A.B - 1;
         const uint8_t* row = stg0 + (gg - r0) * A.stride;  // (a padding row's bytes are zero; it stores nothing)
         int ln = A.rx_len[cg];
@@ -169,13 +171,19 @@ __device__ __forceinline__ void pack_staged(const DelArgs& A, long long grp, con
 // waves a SIMD the register allocation must allow (the SGPR count, 97..112, caps it at 6)
 constexpr int dense_waves(int tb) { return tb <= 6 ? 6 : tb == 7 ? 5 : 3; }
 
-template <int N0, int TB, bool GT = false>
+// G lanes a codeword (round 5: 8, the default -- eight codewords a wave, T / 8 trellises a lane --
+// runs the memoryless subtree's last three levels across lanes instead of four, and a wave
+// instruction serves twice the codewords: C5 848 -> 1009 M cw/s, K = 64 303 -> 452 M, n = 10 77 -> 85 M;
+// 4 lanes measured slower, 943 / 416 M)
+template <int N0, int TB, bool GT = false, int G = kDenseG>
 __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(DelArgs A) {
-    constexpr int L = 1 << N0, T = 1 << TB, G = kDenseG, LV = T / G, CPB = kDenseCPB;
+    constexpr int GB = G == 16 ? 4 : G == 8 ? 3 : 2;
+    static_assert(G == 16 || G == 8 || (G == 4 && TB <= 6), "16 or 8 lanes a codeword, or 4 up to 64 trellises");
+    constexpr int L = 1 << N0, T = 1 << TB, LV = T / G, CPB = kDelBlock / G;
     constexpr int NW = T > 64 ? T / 64 : 1;
     constexpr int WPC = (T * L + 31) / 32;
     constexpr int ROW = N0 == 2 ? kN02Row : kN03Row;
-    constexpr int TL = TB - 4;  // descent levels below the lane's shared prefix
+    constexpr int TL = TB - GB;  // descent levels below the lane's shared prefix
     constexpr uint64_t WM = T >= 64 ? ~0ull : ((1ull << T) - 1ull);
     static_assert((N0 == 2 || N0 == 3) && TB >= 4 && TB <= 8, "dense deletion: n0 2, 3 and 16 .. 256 trellises");
     __shared__ double tab2[N0 == 2 ? kN02States * kN02Row : 1];
@@ -207,7 +215,7 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
     const int lane = threadIdx.x & 63;
     const int j = threadIdx.x & (G - 1);
     const int g = threadIdx.x / G;
-    const uint32_t jr = bitrev((uint32_t)j, 4);
+    const uint32_t jr = bitrev((uint32_t)j, GB);
     const long long ngrp = (A.B + CPB - 1) / CPB;
 #pragma unroll 1
     for (long long grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
@@ -215,9 +223,9 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
         const bool valid = cw < A.B;
         const long long c = valid ? cw : A.B - 1;  // padding codewords decode a duplicate, store nothing
         for (int i = threadIdx.x; i < CPB * WPC; i += kDelBlock) xs[i] = 0;
-        if (dense_stage_bytes(A.stride, A.rx)) {  // received words: staged by 16-byte loads, packed from LDS
-            uint8_t* stg = (uint8_t*)(rxb + dense_stage_off(A.rw));
-            const int R = dense_stage_rows(A.stride);
+        if (dense_stage_bytes(A.stride, A.rx, CPB)) {  // received words: staged by 16-byte loads, packed from LDS
+            uint8_t* stg = (uint8_t*)(rxb + dense_stage_off(A.rw, CPB));
+            const int R = dense_stage_rows(A.stride, CPB);
             for (int r0 = 0; r0 < CPB; r0 += R) {
                 const long long b0 = (grp * CPB + r0) * (long long)A.stride;
                 const long long a0 = b0 & ~15ll;
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
                 if (r0) __syncthreads();  // the previous chunk's rows are packed
                 stage_bytes(A, a0, stg, R * A.stride + mis);
                 __syncthreads();
-                pack_staged(A, grp, stg + mis, r0, R, rxb, lane);
+                pack_staged<CPB>(A, grp, stg + mis, r0, R, rxb, lane);
             }
         } else {
             pack_rows<CPB>(A, grp, rxb, lane);  // received words bit-packed into LDS (sc_del_kern.h)
@@ -238,8 +246,8 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
         int len = A.rx_len[c];
         len = len < 0 ? 0 : (len > A.stride ? A.stride : len);
         int sa[LV], se[LV];
-        dense_segments<TB>(pw, len, jr, sa, se);
-        // local value t (position j + 16 t) is trellis jr * 2^TL + bitrev(t): its state's row
+        dense_segments<TB, GB>(pw, len, jr, sa, se);
+        // local value t (position j + G t) is trellis jr * 2^TL + bitrev(t): its state's row
         int row[LV];
 #pragma unroll
         for (int t = 0; t < LV; ++t) {
@@ -280,7 +288,7 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
                 double v[LV];
 #pragma unroll
                 for (int t = 0; t < LV; ++t) v[t] = tab[row[t] + dense_slot<N0>(k, hist[t])];
-                if constexpr (NW == 1) bits = WinTree<LV, G, 1>::run(v, ub, fm, fv, lane);
+                if constexpr (NW == 1 || G != 16) bits = WinTree<LV, G, NW>::run(v, ub, fm, fv, lane);
                 else bits = DelWin<LV, NW>::run(v, ub, fm, fv, lane);
             }
 #pragma unroll
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
     }
 }
 
-// sc_del_dense.hip; nullptr outside n0 2, 3 and tb 4 .. 8 (gt: n0 = 2 with a built table)
-DelKern del_kernel_dense(int n0, int tb, bool gt = false);
+// sc_del_dense.hip; nullptr outside n0 2, 3 and tb 4 .. 8 (gt: n0 = 2 with a built table; g = 4: tb <= 6)
+DelKern del_kernel_dense(int n0, int tb, bool gt = false, int g = kDenseG);
 
 }  // namespace pcub

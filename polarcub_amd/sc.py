@@ -685,6 +685,16 @@ def leaf_deletion_supported(n, n0, ones=0):
     return bool(_lib.lib().pcub_sc_leaf_deletion_supported(int(n), int(n0), int(ones)))
 
 
+def set_deletion_lanes(g):
+    """Lanes a codeword of the table-driven deletion layout: 8 (default), 16, or 4 (up to 64
+    trellises; 8 beyond) (pcub_sc_set_deletion_lanes); returns the previous value.  Decisions are
+    identical either way."""
+    old = int(_lib.lib().pcub_sc_set_deletion_lanes(int(g)))
+    if old < 0:
+        raise ValueError("deletion lanes: 4, 8 or 16")
+    return old
+
+
 def set_deletion_dense(on):
     """Allow (default) or forbid the table-driven deletion layout (pcub_sc_set_deletion_dense);
     returns the previous setting.  Decisions are identical either way."""

@@ -297,3 +297,39 @@ def test_dense_staging_any_stride(sc, n0, n):
     for i in (0, 22, 44):
         x_ref, i_ref = tro.decode_deletion(words[i], n, n0, 0.1, frozen, fval)
         assert list(ref[0][i]) == i_ref and list(ref[1][i]) == x_ref, i
+
+
+@pytest.mark.parametrize("n0,n", [(2, 6), (2, 7), (2, 8), (3, 7), (3, 8), (3, 9)])
+def test_dense_layout_lanes(sc, n0, n):
+    """The table-driven layout with 16, 8 (the default up to 64 trellises) and 4 lanes a codeword
+    (pcub_sc_set_deletion_lanes: four, three and two cross-lane subtree levels) decodes identically:
+    ragged batch, the n0 = 2 table built per workgroup and given, n0 = 3 with its table; and agrees
+    with the oracle on a sample."""
+    N = 1 << n
+    pd = 0.1
+    rng = np.random.default_rng(5 * n + n0)
+    prng = random.Random(9 * n + n0)
+    frozen = (rng.random(N) < 0.5).astype(np.uint8)
+    frozen[: N // 8] = 1
+    fval = (rng.random(N) < 0.5).astype(np.uint8)
+    words = [tro.deletion_channel(tro.add_guard_bands([int(b) for b in rng.integers(0, 2, N)], n, n0, 0.1, 0), pd, prng)
+             for _ in range(75)]
+    words += [[], [1], [0] * 5, [int(b) for b in rng.integers(0, 2, 2 * N)]]
+    rxt, ln = sc.pad_words(words)
+    code = sc.CodeSpec(N, frozen, fval, device="cuda")
+    for use_table in ((True, False) if n0 == 2 else (True,)):
+        d = sc.DeletionDecoder(code, n0, pd, use_table=use_table)
+        outs = []
+        for g in (16, 8, 4):
+            prev = sc.set_deletion_lanes(g)
+            try:
+                info, xhat = d.decode(rxt, ln)
+                torch.cuda.synchronize()
+            finally:
+                sc.set_deletion_lanes(prev)
+            outs.append((info.cpu().numpy(), xhat.cpu().numpy()))
+        for o in outs[1:]:
+            assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1]), use_table
+    for i in (0, 40, len(words) - 3, len(words) - 1):
+        x_ref, i_ref = tro.decode_deletion(words[i], n, n0, pd, frozen, fval)
+        assert list(outs[1][0][i]) == i_ref and list(outs[1][1][i]) == x_ref, i

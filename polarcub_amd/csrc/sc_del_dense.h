@@ -169,6 +169,8 @@ __device__ __forceinline__ void pack_staged(const DelArgs& A, long long grp, con
 // of each workgroup building it: the build's registers (n02_table_entry) set the kernel's peak
 // (89 -> 79 VGPRs at 64 trellises: 6 waves a SIMD instead of 5)
 // waves a SIMD the register allocation must allow (the SGPR count, 97..112, caps it at 6)
+// (8 lanes a codeword: at 6 waves the 80-VGPR cap spills 61 VGPRs, 148 B a lane, and still wins --
+// C5 1,005 M vs 970 M at 5 waves (96 VGPRs, 26 spilled) and 876 M at 4 (127 VGPRs, none))
 constexpr int dense_waves(int tb) { return tb <= 6 ? 6 : tb == 7 ? 5 : 3; }
 
 // G lanes a codeword (round 5: 8, the default -- eight codewords a wave, T / 8 trellises a lane --

@@ -160,8 +160,42 @@ def build(force=False, verbose=False):
         return _build_locked(force, verbose)
 
 
+TORCH_LIB = os.path.join(LIBDIR, "libpolarcub_torch.so")
+TORCH_SRC = os.path.join(CSRC, "torch", "torch_ops.cpp")
+
+
+def build_torch_ops(force=False, verbose=False):
+    """The PyTorch-ROCm operator library (torch.ops.polarcub.*, csrc/torch/torch_ops.cpp): host-only
+    C++ over the C ABI, linked against libpolarcub_hip.so (found beside it through $ORIGIN)."""
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    flags = ["-O2", "-fPIC", "-shared", "-std=c++17", "-Wall", "-DUSE_ROCM",
+             "-D_GLIBCXX_USE_CXX11_ABI=%d" % int(torch._C._GLIBCXX_USE_CXX11_ABI)]
+    dig = _digest([TORCH_SRC, os.path.join(ROOT, "include", "polarcub_sc.h")], [HIPCC, torch.__version__] + flags)
+    if not force and not _stale(TORCH_LIB, dig):
+        return TORCH_LIB
+    tmp = TORCH_LIB + ".tmp"
+    cmd = ([HIPCC] + flags + ["-I" + os.path.join(tdir, "include"),
+                              "-I" + os.path.join(tdir, "include", "torch", "csrc", "api", "include"),
+                              "-I" + os.path.join(ROOT, "include"), TORCH_SRC, "-o", tmp,
+                              "-L" + os.path.join(tdir, "lib"), "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip",
+                              "-L" + LIBDIR, "-lpolarcub_hip", "-Wl,-rpath,$ORIGIN"])
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, TORCH_LIB)
+    _write_stamp(TORCH_LIB, dig)
+    return TORCH_LIB
+
+
 def _build_locked(force, verbose):
     build_host(force, verbose)
+    lib = _build_hip_locked(force, verbose)
+    build_torch_ops(force, verbose)
+    return lib
+
+
+def _build_hip_locked(force, verbose):
     if not force and up_to_date():
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)

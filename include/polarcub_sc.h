@@ -203,6 +203,11 @@ int pcub_sc_decode_qary_log(const double* xy, int64_t B, int32_t q, int32_t log2
  * CPU-dependent); without ties the final path set and metrics are the reference's.
  * Workspace: pcub_scl_qary_workspace(B, q, log2N, L, K) bytes. */
 size_t pcub_scl_qary_workspace(int64_t B, int32_t q, int32_t log2N, int32_t L, int32_t K);
+/* Kernel layout of the list decoder: 1 = a 64-lane workgroup per codeword (lanes over positions),
+ * 0 = a lane per codeword, -1 = the default (lane mode: measured faster at every shape tried, up to
+ * N = 4096, L = 32).  Both give identical outputs.  Returns the previous setting; size workspaces
+ * after changing it. */
+int pcub_scl_set_wave(int mode);
 int pcub_scl_qary(const double* xy, int64_t B, int32_t q, int32_t log2N, int32_t L, const uint8_t* frozen,
                   const uint8_t* frozen_vals, int32_t nF, const uint8_t* actual, int32_t K, uint8_t* out_info,
                   double* out_prob, int32_t* out_size, double* out_actual, void* workspace, size_t workspace_bytes,

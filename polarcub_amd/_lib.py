@@ -43,6 +43,8 @@ def lib():
     L.pcub_sc_set_max_blocks_per_cu.restype = ctypes.c_int
     L.pcub_sc_set_max_blocks_per_cu.argtypes = [ctypes.c_int]
     L.pcub_sc_set_qary_lanes.restype = ctypes.c_int
+    L.pcub_scl_set_wave.restype = ctypes.c_int
+    L.pcub_scl_set_wave.argtypes = [ctypes.c_int]
     L.pcub_sc_set_qary_lanes.argtypes = [ctypes.c_int]
     L.pcub_sc_set_qary_regs.restype = ctypes.c_int
     L.pcub_sc_set_qary_regs.argtypes = [ctypes.c_int]

@@ -48,7 +48,7 @@ extern "C" {
 
 /* Library version, for the loader's ABI check.  3: the deletion state tables carry an 8-double
  * header (size them with pcub_sc_deletion_table_bytes, never from the version-2 formula), and
- * pcub_tile_pairs. */
+ * pcub_tile_pairs.  4: pcub_scl_set_wave (the list decoder's slower wave-per-codeword layout) removed. */
 int pcub_abi_version(void);
 
 /* Bytes of device workspace pcub_sc_decode_bin needs for a batch of B
@@ -203,11 +203,6 @@ int pcub_sc_decode_qary_log(const double* xy, int64_t B, int32_t q, int32_t log2
  * CPU-dependent); without ties the final path set and metrics are the reference's.
  * Workspace: pcub_scl_qary_workspace(B, q, log2N, L, K) bytes. */
 size_t pcub_scl_qary_workspace(int64_t B, int32_t q, int32_t log2N, int32_t L, int32_t K);
-/* Kernel layout of the list decoder: 1 = a 64-lane workgroup per codeword (lanes over positions),
- * 0 = a lane per codeword, -1 = the default (lane mode: measured faster at every shape tried, up to
- * N = 4096, L = 32).  Both give identical outputs.  Returns the previous setting; size workspaces
- * after changing it. */
-int pcub_scl_set_wave(int mode);
 int pcub_scl_qary(const double* xy, int64_t B, int32_t q, int32_t log2N, int32_t L, const uint8_t* frozen,
                   const uint8_t* frozen_vals, int32_t nF, const uint8_t* actual, int32_t K, uint8_t* out_info,
                   double* out_prob, int32_t* out_size, double* out_actual, void* workspace, size_t workspace_bytes,

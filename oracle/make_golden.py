@@ -1435,6 +1435,141 @@ FIXTURES["deletion_genie_wide"] = fx_deletion_genie_wide
 FIXTURES["scl_log"] = lambda R, t: fx_scl(R, t, use_log=True)
 
 
+# ---------------------------------------------------------------------------
+# edge families at the BASELINE code lengths (N = 1024, 4096)
+# ---------------------------------------------------------------------------
+
+EDGE_LONG_FAMILIES = ("discrete", "subnormal", "random", "one_sided_zeros", "ties", "underflow",
+                      "awgn_2db", "awgn_2db_subnormal_scale", "awgn_high_snr", "awgn_mixed_defects")
+
+
+def _awgn_table(sigma2, levels, scale=1.0):
+    """256-letter quantised BI-AWGN output alphabet: the joint P(x, y) rows at the level centres."""
+    c = 0.5 / math.sqrt(2.0 * math.pi * sigma2)
+    p0 = c * np.exp(-((levels - 1.0) ** 2) / (2.0 * sigma2))
+    p1 = c * np.exp(-((levels + 1.0) ** 2) / (2.0 * sigma2))
+    return np.stack([p0, p1], axis=-1) * scale
+
+
+def _edge_long_inputs(family, N, B, x, rng):
+    """(table [256][2] f64, idx [B][N] u8) for one edge family; xy = table[idx].  x [B][N] is a
+    codeword batch of the case's code (used by the channel-like families)."""
+    vals = np.array([0.0, 0.5, 0.25, 1.0, 0.125, 1e-300, 4.9e-324, 2.2e-308, 0.3, 0.7, 1e-5])
+    idx = rng.integers(0, 256, size=(B, N)).astype(np.uint8)
+    levels = np.linspace(-5.0, 5.0, 256)
+
+    def channel_idx(sigma2):
+        s = 1.0 - 2.0 * x.astype(np.float64)
+        y = s + math.sqrt(sigma2) * rng.standard_normal(x.shape)
+        return np.clip(np.rint((y + 5.0) * 25.5), 0, 255).astype(np.uint8)
+
+    if family == "discrete":        # a few discrete levels: many ties and zeros
+        table = rng.choice(vals[:5], size=(256, 2))
+    elif family == "subnormal":     # subnormal / tiny magnitudes
+        table = rng.choice(vals, size=(256, 2))
+    elif family == "random":
+        table = rng.random((256, 2))
+    elif family == "one_sided_zeros":
+        table = rng.random((256, 2))
+        z = rng.random(256) < 0.3
+        side = rng.integers(0, 2, size=256)
+        table[z, 0] *= side[z]
+        table[z, 1] *= 1 - side[z]
+    elif family == "ties":
+        table = np.repeat(rng.choice(vals[:5], size=(256, 1)), 2, axis=1)
+        flip = rng.random(256) < 0.3
+        table[flip, 1] = rng.random(int(flip.sum()))
+    elif family == "underflow":     # products underflow deep in the tree
+        table = rng.random((256, 2)) * 1e-120
+    elif family == "awgn_2db":      # the C2/C3 channel: the rate-1 shortcut's common case
+        table = _awgn_table(0.630957, levels)
+        idx = channel_idx(0.630957)
+    elif family == "awgn_2db_subnormal_scale":  # root products subnormal (scale 1e-160)
+        table = _awgn_table(0.630957, levels, 1e-160)
+        idx = channel_idx(0.630957)
+    elif family == "awgn_high_snr":  # |LLR| up to ~200 at the levels: ratios underflow to subnormals / 0
+        table = _awgn_table(0.05, levels)
+        idx = channel_idx(0.05)
+    else:                           # awgn_mixed_defects: 2 dB rows with 1 % subnormal / tie / zero letters
+        table = _awgn_table(0.630957, levels)
+        table[0] = (4.9e-324, 0.0)
+        table[1] = (0.0, 4.9e-324)
+        table[2] = (0.0, 0.0)
+        table[3] = (0.25, 0.25)
+        table[4] = (1e-300, 2.2e-308)
+        table[5] = (1.0, 1e-310)
+        idx = channel_idx(0.630957)
+        bad = rng.random((B, N)) < 0.01
+        idx[bad] = rng.integers(0, 6, size=int(bad.sum()))
+    return np.ascontiguousarray(table, np.float64), idx
+
+
+def _edge_long_case(args):
+    """One (N, frozen kind, family) case, decoded by the reference in a worker process."""
+    n, fkind, fam_i, B, seed = args
+    R = _EDGE_R
+    BPED, BMVD = R["BPED"], R["BMVD"]
+    N = 1 << n
+    rng = np.random.default_rng(seed)
+    if fkind == "bhattacharyya":   # the C2 / C3 code: K = N/2 at 2 dB
+        frozen, _ = bhattacharyya_frozen(n, N // 2, 0.630957)
+    else:
+        frozen = set(int(i) for i in np.nonzero(rng.random(N) < 0.5)[0])
+    crs = int(rng.integers(-1, 50))
+    enc = BPED.BinaryPolarEncoderDecoder(N, frozen, crs)
+    u = rng.integers(0, 2, size=(B, enc.k)).astype(np.uint8)
+    x = np.stack([ref_encode(R, N, enc, u[b]) for b in range(B)])
+    table, idx = _edge_long_inputs(EDGE_LONG_FAMILIES[fam_i], N, B, x, rng)
+    xvd = BMVD.BinaryMemorylessVectorDistribution(N)
+    xvd.probs[:] = np.array([0.5, 0.5])
+    info = np.zeros((B, enc.k), np.uint8)
+    xhat = np.zeros((B, N), np.uint8)
+    for b in range(B):
+        xyvd = BMVD.BinaryMemorylessVectorDistribution(N)
+        xyvd.probs[:] = table[idx[b]]
+        xh, inf = enc.decode(xvd, xyvd)
+        info[b] = inf
+        xhat[b] = xh
+    mask, r, fval = frozen_arrays(enc, N)
+    return dict(n=n, family=fam_i, crs=crs, table=table, idx=idx, frozen=mask, fval=fval,
+                info_bits=np.packbits(info, axis=1), xhat_bits=np.packbits(xhat, axis=1), K=enc.k)
+
+
+_EDGE_R = None
+
+
+def fx_edge_long(R, timing):
+    """The six edge families of fx_edge (discrete, subnormal, random, one-sided zeros, ties,
+    underflow) plus four channel-shaped ones (quantised BI-AWGN at 2 dB, the same scaled by 1e-160,
+    a high-SNR channel whose ratios underflow, 2 dB with 1 % defect letters) at N = 1024 and 4096,
+    with the C2 / C3 Bhattacharyya frozen sets and random frozen sets, decoded by the reference
+    (BinaryPolarEncoderDecoder.decode, :71-99).  Inputs are stored as a 256-letter table and u8
+    letter indices (xy = table[idx]); decisions bit-packed along the codeword (np.packbits)."""
+    import multiprocessing as mp
+    global _EDGE_R
+    _EDGE_R = R
+    jobs = []
+    for n, B in ((10, 32), (12, 16)):
+        for fk in ("bhattacharyya", "random"):
+            for fi in range(len(EDGE_LONG_FAMILIES)):
+                jobs.append((n, fk, fi, B, 9000 + 100 * n + 10 * fi + (fk == "random")))
+    t0 = time.time()
+    with mp.get_context("fork").Pool(8) as pool:
+        cases = pool.map(_edge_long_case, jobs, chunksize=1)
+    timing["edge_long_wall_s_8proc"] = time.time() - t0
+    arrays = {}
+    for i, c in enumerate(cases):
+        for k, v in c.items():
+            arrays["c%d_%s" % (i, k)] = np.asarray(v)
+    save("edge_long", dict(cases=len(cases), families=list(EDGE_LONG_FAMILIES),
+                           frozen_kinds=["bhattacharyya (2 dB, K = N/2)", "random 50 %"],
+                           note="xy = table[idx]; info / xhat np.packbits(axis=1); seeds 9000 + 100 n + 10 family "
+                                "+ (random frozen)"), **arrays)
+
+
+FIXTURES["edge_long"] = fx_edge_long
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", nargs="*")

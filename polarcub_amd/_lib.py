@@ -15,7 +15,7 @@ _i32 = ctypes.c_int32
 _lib = None
 
 EINVAL = -1
-ABI_VERSION = 3  # include/polarcub_sc.h (2: guard-band ones in the deletion entry points; 3: table headers, tile_pairs)
+ABI_VERSION = 4  # include/polarcub_sc.h (2: guard-band ones in the deletion entry points; 3: table headers, tile_pairs; 4: pcub_scl_set_wave removed)
 
 
 class HipError(RuntimeError):
@@ -43,8 +43,6 @@ def lib():
     L.pcub_sc_set_max_blocks_per_cu.restype = ctypes.c_int
     L.pcub_sc_set_max_blocks_per_cu.argtypes = [ctypes.c_int]
     L.pcub_sc_set_qary_lanes.restype = ctypes.c_int
-    L.pcub_scl_set_wave.restype = ctypes.c_int
-    L.pcub_scl_set_wave.argtypes = [ctypes.c_int]
     L.pcub_sc_set_qary_lanes.argtypes = [ctypes.c_int]
     L.pcub_sc_set_qary_regs.restype = ctypes.c_int
     L.pcub_sc_set_qary_regs.argtypes = [ctypes.c_int]

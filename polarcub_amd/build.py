@@ -152,12 +152,30 @@ def _compile(src, verbose):
     _write_stamp(obj, dig)
 
 
+class _tree_lock:
+    """One build at a time in this tree (fcntl lock on lib/.build.lock)."""
+
+    def __enter__(self):
+        import fcntl
+        os.makedirs(LIBDIR, exist_ok=True)
+        self.f = open(os.path.join(LIBDIR, ".build.lock"), "w")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *a):
+        self.f.close()
+
+
 def build(force=False, verbose=False):
-    import fcntl
-    os.makedirs(LIBDIR, exist_ok=True)
-    with open(os.path.join(LIBDIR, ".build.lock"), "w") as lock:
-        fcntl.flock(lock, fcntl.LOCK_EX)  # one build at a time in this tree
+    with _tree_lock():
         return _build_locked(force, verbose)
+
+
+def torch_ops_current(verbose=False):
+    """build_torch_ops under the tree lock: rebuilds when torch_ops.cpp, polarcub_sc.h, the
+    compiler or the torch version changed (digest stamp), else returns at once."""
+    with _tree_lock():
+        return build_torch_ops(False, verbose)
 
 
 TORCH_LIB = os.path.join(LIBDIR, "libpolarcub_torch.so")

@@ -13,6 +13,8 @@
 //     nothing, so every wave runs the same schedule.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "polarcub_sc.h"
 #include "sc_bin_kern.h"
 
@@ -27,10 +29,9 @@ extern "C" __attribute__((weak)) void* pcub_exp_kernel(int e, int v, int compact
 static BinKernFn exp_kernel(int e, int v, bool compact) {
     return pcub_exp_kernel ? (BinKernFn)pcub_exp_kernel(e, v, compact ? 1 : 0) : nullptr;
 }
-static int g_experiment = 0;
+static std::atomic<int> g_experiment{0};
 extern "C" int pcub_sc_set_experiment(int e) {
-    const int old = g_experiment;
-    g_experiment = e;
+    const int old = g_experiment.exchange(e);
     return old;
 }
 // the selected experiment, for the q-ary launcher's hook (sc_qary.hip)
@@ -167,7 +168,7 @@ int pick_variant(int n) {
 
 }  // namespace
 
-extern "C" int pcub_abi_version(void) { return 3; }
+extern "C" int pcub_abi_version(void) { return 4; }
 
 // Tuning hooks (not part of the stable ABI): choose / describe the decode kernel variant.
 extern "C" int pcub_sc_num_variants(void) { return kNumVariants; }

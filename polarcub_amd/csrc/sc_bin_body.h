@@ -299,12 +299,12 @@ PCUB_HD uint32_t rate1_node(const double* v, uint64_t& ub, int lane) {
 
 // Register-resident virtual subtree of L values per lane; virtual leaf BASE_V
 // covers real u positions [BASE_V*G, BASE_V*G + G).  Returns L local encoding bits.
-template <int L, int BASE_V, int G>
+// R1: try the rate-1 shortcut (the deletion kernels choose: their rows hold ties and (0, 0) pairs;
+// the 16-lane layout never qualifies, G <= 8, and the 8-lane one measured it)
+template <int L, int BASE_V, int G, bool R1 = true>
 struct SubV {
     static PCUB_HD uint32_t run(const double* v, uint64_t& ub, uint64_t fm, uint64_t fv, int lane) {
-        // (not in the deletion kernels' 16-lane subtrees: their rows hold ties and (0, 0) pairs, and
-        // there the test cost more than it saved -- C5 853 -> 820 M cw/s, K = 64 305 -> 298 M)
-        if constexpr (L >= 2 && L * G >= 16 && G <= 8) {
+        if constexpr (R1 && L >= 2 && L * G >= 16 && G <= 8) {
             // a rate-1 node (no frozen position; wave-uniform) whose codewords all pass the test
             constexpr uint64_t NM = (L * G == 64) ? ~0ull : ((1ull << (L * G)) - 1ull);
             if (((fm >> (BASE_V * G)) & NM) == 0ull && rate1_sure<L, G>(v)) return rate1_node<L, BASE_V, G>(v, ub, lane);
@@ -336,7 +336,7 @@ struct SubV {
             } else {
 #pragma unroll
                 for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
-                ym = SubV<H, BASE_V, G>::run(c, ub, fm, fv, lane);
+                ym = SubV<H, BASE_V, G, R1>::run(c, ub, fm, fv, lane);
             }
             if (all_frozen<HR>(fm, (BASE_V + H) * G)) {
                 yp = frozen_local<H, G>(fv >> ((BASE_V + H) * G), j) & LMASK;
@@ -344,7 +344,7 @@ struct SubV {
             } else {
 #pragma unroll
                 for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
-                yp = SubV<H, BASE_V + H, G>::run(c, ub, fm, fv, lane);
+                yp = SubV<H, BASE_V + H, G, R1>::run(c, ub, fm, fv, lane);
             }
             return (ym ^ yp) | (yp << H);
         }
@@ -538,11 +538,11 @@ PCUB_HD void sched_fence() {
 // A register subtree's u decisions and frozen bits live in NW 64-bit windows
 // (NW = S*G/64 when the subtree has more than 64 real positions): WinTree splits
 // the subtree at its top nodes until each part is one window.
-template <int L, int G, int NWIN>
+template <int L, int G, int NWIN, bool R1 = true>
 struct WinTree {
     static PCUB_HD uint32_t run(const double* v, uint64_t* ub, const uint64_t* fm, const uint64_t* fv, int lane) {
         if constexpr (NWIN == 1) {
-            return SubV<L, 0, G>::run(v, ub[0], fm[0], fv[0], lane);
+            return SubV<L, 0, G, R1>::run(v, ub[0], fm[0], fv[0], lane);
         } else {
             constexpr int H = L / 2;
             constexpr int HW = NWIN / 2;
@@ -553,14 +553,14 @@ struct WinTree {
             } else {
 #pragma unroll
                 for (int t = 0; t < H; ++t) c[t] = op_f(v[t], v[t + H]);
-                ym = WinTree<H, G, HW>::run(c, ub, fm, fv, lane);
+                ym = WinTree<H, G, HW, R1>::run(c, ub, fm, fv, lane);
             }
             if (frozen_windows(fm + HW)) {
                 yp = WinTree<H, G, HW>::frozen(ub + HW, fv + HW, lane & (G - 1));
             } else {
 #pragma unroll
                 for (int t = 0; t < H; ++t) c[t] = op_g(v[t], v[t + H], (ym >> t) & 1u);
-                yp = WinTree<H, G, HW>::run(c, ub + HW, fm + HW, fv + HW, lane);
+                yp = WinTree<H, G, HW, R1>::run(c, ub + HW, fm + HW, fv + HW, lane);
             }
             return (ym ^ yp) | (yp << H);
         }

@@ -28,6 +28,7 @@ constexpr int kMaxOnes = 3;
 constexpr int kMaxStride = 1 << 24;
 
 std::atomic<int> g_dense{1};  // the table-driven layout allowed (pcub_sc_set_deletion_dense)
+std::atomic<int> g_dense_rate1{1};  // the 8-lane layout's rate-1 shortcut (pcub_sc_set_deletion_rate1)
 std::atomic<int> g_dense_lanes{8};  // lanes a codeword of the table-driven layout (8, 16; 4 up to 64 trellises)
 
 // Status words of table-checked launches (one ring per device; sc_del_kern.h, DelArgs::gate): a
@@ -196,6 +197,10 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     }
     const int dg = dense_lanes(n - n0);
     DelKern k = dense ? del_kernel_dense(n0, n - n0, n0 == 2 && A.tab, dg) : kern;
+    if (dense && dg == 8 && !g_dense_rate1.load(std::memory_order_relaxed)) {
+        DelKern k0 = del_kernel_dense(n0, n - n0, n0 == 2 && A.tab, dg, false);
+        if (k0) k = k0;
+    }
     // the general kernel's workgroup: 256 threads, or T for 512 / 1024 trellises (one codeword)
     const int blk = dense ? kDelBlock : ((n - n0) > 8 ? 1 << (n - n0) : kDelBlock);
     long long cpb = dense ? kDelBlock / dg : blk >> (n - n0);
@@ -281,6 +286,11 @@ extern "C" int pcub_sc_set_deletion_lanes(int32_t g) {
     if (g != 4 && g != 8 && g != 16) return -1;
     return g_dense_lanes.exchange(g);
 }
+
+// Diagnostic (not part of the stable ABI): 0 runs the 8-lane table-driven kernel's subtrees without
+// the rate-1 shortcut where such a twin is built (n0 = 2 with a table, 64 / 256 trellises); the A/B
+// of DESIGN 3.2.  Decisions are identical either way.  Returns the previous setting.
+extern "C" int pcub_sc_set_deletion_rate1(int32_t on) { return g_dense_rate1.exchange(on ? 1 : 0); }
 
 extern "C" int pcub_sc_set_deletion_dense(int32_t on) {
     return g_dense.exchange(on ? 1 : 0);

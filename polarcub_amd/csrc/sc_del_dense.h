@@ -177,7 +177,25 @@ constexpr int dense_waves(int tb) { return tb <= 6 ? 6 : tb == 7 ? 5 : 3; }
 // runs the memoryless subtree's last three levels across lanes instead of four, and a wave
 // instruction serves twice the codewords: C5 848 -> 1009 M cw/s, K = 64 303 -> 452 M, n = 10 77 -> 85 M;
 // 4 lanes measured slower, 943 / 416 M)
-template <int N0, int TB, bool GT = false, int G = kDenseG>
+// A trellis's state row and decision history share one packed field: (row << HB) | history, HB = 2^n0
+// history bits; n0 = 2 (row < 2^10) packs two trellises a 32-bit word, n0 = 3 (row < 2^18) one.  The
+// 8-lane layout holds LV = T / 8 trellises a lane, and the unpacked row[] / hist[] pairs (2 LV VGPRs)
+// were a large part of what spilled at the 80-VGPR cap of 6 waves a SIMD.
+template <int N0, int LV>
+struct RowHist {
+    static constexpr int HB = 1 << N0;                     // history bits
+    static constexpr int PER = N0 == 2 ? 2 : 1;            // trellises a word
+    static constexpr int FB = 32 / PER;                    // field bits
+    static constexpr uint32_t FM = PER == 1 ? ~0u : ((1u << FB) - 1u);
+    uint32_t w[(LV + PER - 1) / PER];
+    PCUB_HD uint32_t field(int t) const { return (w[t / PER] >> (FB * (t % PER))) & FM; }
+    PCUB_HD int row(int t) const { return (int)(field(t) >> HB); }
+    PCUB_HD uint32_t hist(int t) const { return field(t) & ((1u << HB) - 1u); }
+    PCUB_HD void set_row(int t, int r) { w[t / PER] |= ((uint32_t)r << HB) << (FB * (t % PER)); }
+    PCUB_HD void add_bit(int t, uint32_t b, int k) { w[t / PER] |= (b << k) << (FB * (t % PER)); }
+};
+
+template <int N0, int TB, bool GT = false, int G = kDenseG, bool R1 = true>
 __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(DelArgs A) {
     constexpr int GB = G == 16 ? 4 : G == 8 ? 3 : 2;
     static_assert(G == 16 || G == 8 || (G == 4 && TB <= 6), "16 or 8 lanes a codeword, or 4 up to 64 trellises");
@@ -249,20 +267,20 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
         len = len < 0 ? 0 : (len > A.stride ? A.stride : len);
         int sa[LV], se[LV];
         dense_segments<TB, GB>(pw, len, jr, sa, se);
-        // local value t (position j + G t) is trellis jr * 2^TL + bitrev(t): its state's row
-        int row[LV];
+        // local value t (position j + G t) is trellis jr * 2^TL + bitrev(t): its state's row; the
+        // walk's decision history (empty) beside it
+        RowHist<N0, LV> rh;
+#pragma unroll
+        for (int i = 0; i < (LV + RowHist<N0, LV>::PER - 1) / RowHist<N0, LV>::PER; ++i) rh.w[i] = 0;
 #pragma unroll
         for (int t = 0; t < LV; ++t) {
             const int i = cbitrev(t, TL);
             const int s = sa[i], m = se[i] - sa[i];
             const uint32_t y = m <= L ? packed_bits(pw, s, m, A.rw) : 0u;
-            row[t] = (N0 == 2 ? n02_state(m, y) : n03_state(m, y)) * ROW;
+            rh.set_row(t, (N0 == 2 ? n02_state(m, y) : n03_state(m, y)) * ROW);
         }
 
         // the walk: 2^n0 memoryless subtrees, input k of each trellis from its row and history
-        uint32_t hist[LV];
-#pragma unroll
-        for (int t = 0; t < LV; ++t) hist[t] = 0;
         uint32_t acc = 0;
         int nacc = 0, infow = 0;
 #pragma unroll 1
@@ -289,12 +307,12 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
             } else {
                 double v[LV];
 #pragma unroll
-                for (int t = 0; t < LV; ++t) v[t] = tab[row[t] + dense_slot<N0>(k, hist[t])];
-                if constexpr (NW == 1 || G != 16) bits = WinTree<LV, G, NW>::run(v, ub, fm, fv, lane);
+                for (int t = 0; t < LV; ++t) v[t] = tab[rh.row(t) + dense_slot<N0>(k, rh.hist(t))];
+                if constexpr (NW == 1 || G != 16) bits = WinTree<LV, G, NW, R1>::run(v, ub, fm, fv, lane);
                 else bits = DelWin<LV, NW>::run(v, ub, fm, fv, lane);
             }
 #pragma unroll
-            for (int t = 0; t < LV; ++t) hist[t] |= ((bits >> t) & 1u) << k;
+            for (int t = 0; t < LV; ++t) rh.add_bit(t, (bits >> t) & 1u, k);
             // information bits in u order (lane j = 0 holds the subtree's decisions)
 #pragma unroll
             for (int w = 0; w < NW; ++w) {
@@ -315,7 +333,7 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
 #pragma unroll
         for (int t = 0; t < LV; ++t) {
             const int pos = (int)((jr << TL) | (uint32_t)cbitrev(t, TL)) * L;
-            atomicOr(&xs[g * WPC + (pos >> 5)], enc_hist<L>(hist[t]) << (pos & 31));
+            atomicOr(&xs[g * WPC + (pos >> 5)], enc_hist<L>(rh.hist(t)) << (pos & 31));
         }
         __syncthreads();
         if (A.xhat && valid)
@@ -324,7 +342,8 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
     }
 }
 
-// sc_del_dense.hip; nullptr outside n0 2, 3 and tb 4 .. 8 (gt: n0 = 2 with a built table; g = 4: tb <= 6)
-DelKern del_kernel_dense(int n0, int tb, bool gt = false, int g = kDenseG);
+// sc_del_dense.hip; nullptr outside n0 2, 3 and tb 4 .. 8 (gt: n0 = 2 with a built table; g = 4: tb <= 6);
+// r1 = false: the subtrees without the rate-1 shortcut (8 lanes a codeword only)
+DelKern del_kernel_dense(int n0, int tb, bool gt = false, int g = kDenseG, bool r1 = true);
 
 }  // namespace pcub

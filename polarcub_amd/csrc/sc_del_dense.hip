@@ -3,7 +3,7 @@
 
 namespace pcub {
 
-DelKern del_kernel_dense(int n0, int tb, bool gt, int g) {
+DelKern del_kernel_dense(int n0, int tb, bool gt, int g, bool r1) {
 #define PCUB_DENSE(N0, GT)                             \
     switch (tb) {                                      \
         case 4: return k_sc_del_dense<N0, 4, GT>;      \
@@ -28,6 +28,16 @@ DelKern del_kernel_dense(int n0, int tb, bool gt, int g) {
         case 7: return k_sc_del_dense<N0, 7, GT, 8>;   \
         case 8: return k_sc_del_dense<N0, 8, GT, 8>;   \
         default: return nullptr;                       \
+    }
+    if (g == 8 && !r1) {  // the rate-1 A/B (pcub_sc_set_deletion_rate1, a diagnostic)
+        if (n0 == 2 && gt) {
+            switch (tb) {
+                case 6: return k_sc_del_dense<2, 6, true, 8, false>;
+                case 8: return k_sc_del_dense<2, 8, true, 8, false>;
+                default: return nullptr;
+            }
+        }
+        return nullptr;
     }
     if (g == 8) {
         if (n0 == 2 && gt) PCUB_DENSE_8(2, true)

@@ -6,18 +6,13 @@
 // same recursion, touch consecutive words).  The recursion is a loop over an explicit frame
 // stack (scl_run), so the kernel has a fixed private segment and no dynamic stack: the launch
 // never depends on the device's per-thread stack limit, and the library never changes it.
-// Wave mode (k_scl_wave, pcub_scl_set_wave(1)): one 64-lane workgroup per codeword, the lanes
-// splitting the transforms' and the combine's position loops over a slot-major slab and running
-// the forks, prunes and special nodes in lockstep (the same values on every lane).  Its slab is
-// 64x smaller than lane mode's full grid, but the special nodes stay serial per codeword and only
-// 16 codewords a CU are in flight: measured 0.66 k vs 1.65 k cw/s at q = 4, N = 4096, L = 32
-// (DESIGN §3.6), so lane mode stays the default.
+// (A wave-per-codeword layout with lanes over positions was measured in round 5 at 0.66 k vs
+// 1.65 k cw/s at q = 4, N = 4096, L = 32 and removed)
 // List decoding is a host-side tool in the reference
 // (the IR simulation); the kernel batches it, it is not the SC throughput path.
 #include <hip/hip_runtime.h>
 
 #include "polarcub_sc.h"
-#define PCUB_SCL_SYNC() __syncthreads()
 #include "scl_body.h"
 
 using namespace pcub;
@@ -36,35 +31,23 @@ __global__ __launch_bounds__(kSclBlock) void k_scl(SclArgs A) {
     }
 }
 
-__global__ __launch_bounds__(kSclBlock) void k_scl_wave(SclArgs A) {
-    for (long long cw = blockIdx.x; cw < A.B; cw += gridDim.x)
-        scl_decode_cw(A, cw, blockIdx.x, true, (int)threadIdx.x, kSclBlock);
-}
-
-int g_scl_wave = -1;  // -1: the default (lane mode); 0: lane mode; 1: wave mode
-
-bool scl_wave(int32_t) { return g_scl_wave > 0; }
-
 bool scl_args_ok(int64_t B, int32_t q, int32_t log2N, int32_t L, int32_t K) {
     return B >= 0 && q >= 2 && q <= 8 && log2N >= 0 && log2N <= 12 && L >= 1 && L <= 64 && K >= 0 &&
            K <= (1 << log2N);
 }
 
-// workgroups of a launch: lane mode 8 a CU (64 codewords each), wave mode 16 a CU (one each)
-long long scl_grid(long long B, bool wave) {
+// workgroups of a launch: 8 a CU (64 codewords each)
+long long scl_grid(long long B) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    const long long ntiles = wave ? B : (B + kSclBlock - 1) / kSclBlock;
-    const long long g = (long long)cus * (wave ? 16 : 8);
+    const long long ntiles = (B + kSclBlock - 1) / kSclBlock;
+    const long long g = (long long)cus * 8;
     return ntiles < g ? ntiles : g;
 }
 
-// slots (codewords in flight) of a launch: lane mode kSclBlock per workgroup, wave mode one
-long long scl_slots(long long B, int32_t log2N) {
-    const long long g = scl_grid(B, scl_wave(log2N));
-    return scl_wave(log2N) ? g : g * kSclBlock;
-}
+// slots (codewords in flight) of a launch: kSclBlock per workgroup
+long long scl_slots(long long B) { return scl_grid(B) * kSclBlock; }
 
 size_t scl_slot_bytes(int32_t q, int32_t log2N, int32_t L, int32_t K) {
     SclLayout Y;
@@ -76,14 +59,7 @@ size_t scl_slot_bytes(int32_t q, int32_t log2N, int32_t L, int32_t K) {
 
 extern "C" size_t pcub_scl_qary_workspace(int64_t B, int32_t q, int32_t log2N, int32_t L, int32_t K) {
     if (B <= 0 || !scl_args_ok(B, q, log2N, L, K)) return 0;
-    return (size_t)scl_slots(B, log2N) * scl_slot_bytes(q, log2N, L, K) + 16;
-}
-
-// 1: wave mode, 0: lane mode, -1: by code length (the default); returns the previous setting
-extern "C" int pcub_scl_set_wave(int mode) {
-    const int old = g_scl_wave;
-    g_scl_wave = mode < 0 ? -1 : (mode ? 1 : 0);
-    return old;
+    return (size_t)scl_slots(B) * scl_slot_bytes(q, log2N, L, K) + 16;
 }
 
 namespace {
@@ -96,10 +72,9 @@ int launch_scl(bool lg, const double* xy, int64_t B, int32_t q, int32_t log2N, i
     if (B == 0) return 0;
     if (!xy || (nF > 0 && !frozen_vals) || !out_info || !out_prob || !out_size || !workspace) return PCUB_EINVAL;
     if (actual && !out_actual) return PCUB_EINVAL;
-    const bool wave = scl_wave(log2N);
-    long long g = scl_grid(B, wave);
+    long long g = scl_grid(B);
     if (g <= 0) return (int)hipErrorNoDevice;
-    const size_t per_block = (size_t)(wave ? 1 : kSclBlock) * scl_slot_bytes(q, log2N, L, K);
+    const size_t per_block = (size_t)kSclBlock * scl_slot_bytes(q, log2N, L, K);
     if ((size_t)g * per_block > workspace_bytes) g = (long long)(workspace_bytes / per_block);
     if (g <= 0) return PCUB_EINVAL;
     SclLayout Y;
@@ -120,13 +95,10 @@ int launch_scl(bool lg, const double* xy, int64_t B, int32_t q, int32_t log2N, i
     A.out_size = (int*)out_size;
     A.out_actual = out_actual;
     A.log = lg ? 1 : 0;
-    A.ns = wave ? g : g * kSclBlock;
+    A.ns = g * kSclBlock;
     A.cells = (double*)workspace;
     A.bytes = (uint8_t*)workspace + (size_t)Y.ncells * 8 * (size_t)A.ns;
-    if (wave)
-        hipLaunchKernelGGL(k_scl_wave, dim3((unsigned)g), dim3(kSclBlock), 0, (hipStream_t)stream, A);
-    else
-        hipLaunchKernelGGL(k_scl, dim3((unsigned)g), dim3(kSclBlock), 0, (hipStream_t)stream, A);
+    hipLaunchKernelGGL(k_scl, dim3((unsigned)g), dim3(kSclBlock), 0, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
 

@@ -57,12 +57,6 @@
 #ifndef PCUB_SCL_FRAME
 #define PCUB_SCL_FRAME()
 #endif
-// wave mode (one codeword per 64-lane workgroup, scl.hip's k_scl_wave): the lanes split the
-// position loops of the transforms and the combine, so their slab writes must be visible to the
-// whole wave before the next step reads them.  scl.hip defines it as the workgroup barrier.
-#ifndef PCUB_SCL_SYNC
-#define PCUB_SCL_SYNC()
-#endif
 
 namespace pcub {
 
@@ -133,7 +127,6 @@ struct SclCtx {
     bool track;      // actual path present
     bool lg;         // log domain
     double actual_prob;
-    int lane, nl;    // wave mode: this lane and the lanes sharing the codeword (lane mode: 0, 1)
 
     PCUB_HD double& C(long long e) {
         PCUB_SCL_TOUCH(8);
@@ -584,7 +577,7 @@ PCUB_HD void scl_store_log(SclCtx& c, int d, int slot, int h, const double* o) {
 PCUB_HD void scl_minus(SclCtx& c, int d, int slot_in, int slot_out) {
     const SclLayout& Y = c.Y;
     const int q = Y.q, H = (Y.N >> d) / 2;
-    for (int h = c.lane; h < H; h += c.nl) {
+    for (int h = 0; h < H; ++h) {
         double o[8];
         if (c.lg) {
             for (int u = 0; u < q; ++u) o[u] = -INFINITY;
@@ -613,7 +606,7 @@ PCUB_HD void scl_minus(SclCtx& c, int d, int slot_in, int slot_out) {
 PCUB_HD void scl_plus(SclCtx& c, int d, int slot_in, int slot_out, long long encm) {
     const SclLayout& Y = c.Y;
     const int q = Y.q, H = (Y.N >> d) / 2;
-    for (int h = c.lane; h < H; h += c.nl) {
+    for (int h = 0; h < H; ++h) {
         const int u1 = c.Bt(encm + h);
         double o[8];
         if (c.lg) {
@@ -641,7 +634,7 @@ PCUB_HD void scl_combine(SclCtx& c, int d, int side, int Lp, int* origin) {
     const long long mapm = Y.c_map + (long long)(d + 1) * L;
     for (int r = 0; r < Lp; ++r) {
         const int mi = (int)c.C(mapm + r);
-        for (int h = c.lane; h < H; h += c.nl) {
+        for (int h = 0; h < H; ++h) {
             const int xm = c.Bt(Y.enc(d + 1, 0, mi, h)), xp = c.Bt(Y.enc(d + 1, 1, r, h));
             c.Bt(Y.enc(d, side, r, 2 * h)) = (uint8_t)((xm + xp) % q);
             c.Bt(Y.enc(d, side, r, 2 * h + 1)) = (uint8_t)((q - xp) % q);
@@ -650,7 +643,7 @@ PCUB_HD void scl_combine(SclCtx& c, int d, int side, int Lp, int* origin) {
     }
     for (int r = 0; r < Lp; ++r) c.C(mapo + r) = (double)origin[r];
     if (c.track)
-        for (int h = c.lane; h < H; h += c.nl) {
+        for (int h = 0; h < H; ++h) {
             const int xm = c.Bt(Y.enc(d + 1, 0, L, h)), xp = c.Bt(Y.enc(d + 1, 1, L, h));
             c.Bt(Y.enc(d, side, L, 2 * h)) = (uint8_t)((xm + xp) % q);
             c.Bt(Y.enc(d, side, L, 2 * h + 1)) = (uint8_t)((q - xp) % q);
@@ -681,15 +674,12 @@ PCUB_HD int scl_run(SclCtx& c) {
         if (f.phase == 0) {
             const int nin = scl_nin(c, f.u0, S);
             if (scl_is_special(S, nin)) {
-                if (c.nl > 1) PCUB_SCL_SYNC();  // every lane done reading what the node rewrites
                 ret = scl_special(c, f.d, f.u0, f.ii, f.side, f.Lin, nin, origin);
-                if (c.nl > 1) PCUB_SCL_SYNC();
                 --sp;
                 continue;
             }
             for (int i = 0; i < f.Lin; ++i) scl_minus(c, f.d, f.d == 0 ? 0 : i, i);
             if (c.track) scl_minus(c, f.d, f.d == 0 ? 0 : L, L);
-            if (c.nl > 1) PCUB_SCL_SYNC();
             f.phase = 1;
             st[sp + 1] = SclFrame{f.d + 1, f.u0, f.ii, 0, f.Lin, 0};
             ++sp;
@@ -698,43 +688,30 @@ PCUB_HD int scl_run(SclCtx& c) {
             const long long save = Y.c_save + (long long)f.d * L;
             const long long mapm = Y.c_map + (long long)(f.d + 1) * L;
             for (int r = 0; r < Lm; ++r) c.C(save + r) = c.C(mapm + r);
-            if (c.nl > 1) PCUB_SCL_SYNC();  // every lane read mapm before a special child rewrites it
             const int iim = f.ii + scl_nin(c, f.u0, H);
             for (int r = 0; r < Lm; ++r) scl_plus(c, f.d, f.d == 0 ? 0 : (int)c.C(save + r), r, Y.enc(f.d + 1, 0, r, 0));
             if (c.track) scl_plus(c, f.d, f.d == 0 ? 0 : L, L, Y.enc(f.d + 1, 0, L, 0));
-            if (c.nl > 1) PCUB_SCL_SYNC();
             f.phase = 2;
             st[sp + 1] = SclFrame{f.d + 1, f.u0 + H, iim, 1, Lm, 0};
             ++sp;
         } else {
             scl_combine(c, f.d, f.side, ret, origin);  // ret = the plus child's list size = this node's
-            if (c.nl > 1) PCUB_SCL_SYNC();
             --sp;
         }
     }
     return ret;
 }
 
-// decode codeword cw with slab slot `slot`; store = false for padding lanes.  Lane mode (nl = 1):
-// the slab is slot-minor (element e of slot s at [e * ns + s]).  Wave mode (nl = 64 lanes on one
-// codeword, lane = this lane): slot-major (element e at [s * ncells + e]), so lanes over positions
-// touch consecutive words.
-PCUB_HD void scl_decode_cw(const SclArgs& A, long long cw, long long slot, bool store, int lane = 0, int nl = 1) {
+// decode codeword cw with slab slot `slot`; store = false for padding lanes.  The slab is
+// slot-minor (element e of slot s at [e * ns + s]).
+PCUB_HD void scl_decode_cw(const SclArgs& A, long long cw, long long slot, bool store) {
     SclCtx c;
     c.A = &A;
     c.Y.init(A.n, A.q, A.L, A.K);
     c.cw = cw;
-    c.lane = lane;
-    c.nl = nl;
-    if (nl > 1) {
-        c.cells = A.cells + slot * c.Y.ncells;
-        c.bytes = A.bytes + slot * c.Y.nbytes;
-        c.ns = 1;
-    } else {
-        c.cells = A.cells + slot;
-        c.bytes = A.bytes + slot;
-        c.ns = A.ns;
-    }
+    c.cells = A.cells + slot;
+    c.bytes = A.bytes + slot;
+    c.ns = A.ns;
     c.fi = 0;
     c.buf = 0;
     c.track = A.actual != nullptr;
@@ -747,7 +724,7 @@ PCUB_HD void scl_decode_cw(const SclArgs& A, long long cw, long long slot, bool 
     A.out_size[cw] = k;
     for (int r = 0; r < A.L; ++r) {
         A.out_prob[(long long)r * B + cw] = r < k ? c.C(c.Y.c_prob + r) : 0.0;
-        for (int j = lane; j < A.K; j += nl)
+        for (int j = 0; j < A.K; ++j)
             A.out_info[((long long)r * A.K + j) * B + cw] = r < k ? c.Bt(c.Y.info(c.buf, r, j)) : (uint8_t)0xff;
     }
     if (c.track && A.out_actual) A.out_actual[cw] = c.actual_prob;

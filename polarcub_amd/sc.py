@@ -131,12 +131,6 @@ def set_max_blocks_per_cu(b):
     _lib.check(_lib.lib().pcub_sc_set_max_blocks_per_cu(int(b)), "pcub_sc_set_max_blocks_per_cu")
 
 
-def set_scl_wave(mode=-1):
-    """List decoder layout: 1 = a 64-lane workgroup per codeword, 0 = a lane per codeword, -1 = the
-    default (lane mode, measured faster).  Identical outputs.  Returns the previous setting."""
-    return int(_lib.lib().pcub_scl_set_wave(int(mode)))
-
-
 def set_qary_lanes(g):
     """Lanes per codeword of the q-ary decode kernel (1, 2, 4, 8 or 16; reduced for
     short codes; 8 and 16 only where instantiated, else 4).  Returns the previous setting."""

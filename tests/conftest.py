@@ -31,6 +31,28 @@ def edge_cases():
     return cases
 
 
+_EDGE_LONG = None
+
+
+def edge_long_cases():
+    """tests/golden/edge_long.npz (oracle/make_golden.py fx_edge_long): the reference's decodes of
+    the edge families at N = 1024 / 4096, unpacked to xy [B][N][2], info [B][K], xhat [B][N]."""
+    global _EDGE_LONG
+    if _EDGE_LONG is None:
+        g = load_golden("edge_long")
+        cases = []
+        for i in range(g["meta"]["cases"]):
+            c = {k.split("_", 1)[1]: v for k, v in g.items() if k.startswith("c%d_" % i)}
+            N, K = 1 << int(c["n"]), int(c["K"])
+            c["xy"] = c["table"][c["idx"]]
+            c["info"] = np.unpackbits(c["info_bits"], axis=1)[:, :K]
+            c["xhat"] = np.unpackbits(c["xhat_bits"], axis=1)[:, :N]
+            c["family_name"] = g["meta"]["families"][int(c["family"])]
+            cases.append(c)
+        _EDGE_LONG = cases
+    return _EDGE_LONG
+
+
 @pytest.fixture(scope="session")
 def golden():
     return load_golden

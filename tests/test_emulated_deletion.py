@@ -179,7 +179,7 @@ def test_wide_shapes_vs_oracle(n0, n, ones, implicit_base):
 
 
 def test_dense_trellis_matches_trel():
-    """trellis_dense.h (the dense-slot trellises of the n0 >= 3 decode path, no guard-band ones)
+    """trellis_dense.h (the dense-slot trellises, test-only: tests/emu/, no guard-band ones)
     against trellis_body.h's Trel on random segments (n0 = 3 and 4, pd from 0 to 1, lengths around,
     below and above the trellis length) and random decision histories: every stage holds the same
     edges in the same creation order, the same vertices in the same insertion order, bit-identical

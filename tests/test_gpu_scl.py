@@ -138,18 +138,8 @@ def test_gpu_list_decoder_workspace_capped(sc):
                                                                                fv[:, idx].contiguous())
     assert torch.equal(size[idx], size1)
     assert torch.equal(info[:, :, idx], info1) and torch.equal(prob[:, idx], prob1)
-    old = sc.set_scl_wave(0)
-    try:
-        big = int(_lib.lib().pcub_scl_qary_workspace(1 << 17, 4, 12, 32, 2048))
-    finally:
-        sc.set_scl_wave(old)
-    assert big > torch.cuda.get_device_properties(0).total_memory  # why the cap exists (lane mode)
-    old = sc.set_scl_wave(1)
-    try:
-        wave = int(_lib.lib().pcub_scl_qary_workspace(1 << 17, 4, 12, 32, 2048))
-    finally:
-        sc.set_scl_wave(old)
-    assert wave < torch.cuda.get_device_properties(0).total_memory // 4  # wave mode: 16 slots a CU
+    big = int(_lib.lib().pcub_scl_qary_workspace(1 << 17, 4, 12, 32, 2048))
+    assert big > torch.cuda.get_device_properties(0).total_memory  # why the cap exists
     d0 = sc.QaryListDecoder(2, 16, np.zeros(16, np.uint8), 4)
     i0, p0, s0, _ = d0.decode(rng.random((3, 16, 2)), np.zeros((3, 0), np.uint8))
     assert i0.shape == (3, 4, 16) and (s0 >= 1).all()
@@ -261,34 +251,3 @@ def test_gpu_list_decoder_n4096_l32_capped(sc):
         assert int(size[b]) == k
         assert info[:k, :, b].cpu().numpy().tolist() == oinfo
         assert np.array_equal(prob[:k, b].cpu().numpy(), np.array(oprob))
-
-
-@pytest.mark.parametrize("q,n,L", [(4, 8, 8), (2, 10, 4), (4, 10, 16), (3, 6, 5)])
-def test_gpu_list_decoder_wave_mode_matches_lane_mode(q, n, L):
-    """k_scl_wave (a workgroup per codeword, lanes over positions, slot-major slab) gives the same
-    lists, metrics, sizes and actual_prob as k_scl (a lane per codeword) on the same inputs."""
-    import torch
-    from polarcub_amd import sc as _sc
-    rng = np.random.default_rng(100 * n + L)
-    N, B = 1 << n, 150
-    frozen = np.zeros(N, np.uint8)
-    frozen[rng.permutation(N)[: N // 2]] = 1
-    nF = int(frozen.sum())
-    p = 0.15
-    tab = np.full((q, q), p / (q - 1))
-    np.fill_diagonal(tab, 1 - p)
-    x = rng.integers(0, q, (B, N))
-    y = np.where(rng.random((B, N)) < p, (x + rng.integers(1, q, (B, N))) % q, x)
-    xy = torch.from_numpy(np.ascontiguousarray((tab[y] / q).transpose(1, 0, 2))).cuda()
-    fv = torch.from_numpy(rng.integers(0, q, (nF, B)).astype(np.uint8)).cuda()
-    act = torch.from_numpy(rng.integers(0, q, (N - nF, B)).astype(np.uint8)).cuda()
-    outs = []
-    for mode in (0, 1):
-        old = _sc.set_scl_wave(mode)
-        try:
-            outs.append(_sc.QaryListDecoder(q, N, frozen, L).decode_native(xy, fv, act))
-            torch.cuda.synchronize()
-        finally:
-            _sc.set_scl_wave(old)
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from oracle import orc
-from tests.conftest import edge_cases, load_golden
+from tests.conftest import edge_cases, edge_long_cases, load_golden
 
 BIN_SETS = ["bsc_n64", "awgn_n1024", "awgn_n4096", "awgn_n256_lowsnr"]
 
@@ -49,6 +49,16 @@ def test_edge_cases(idx):
         i2, x2, _ = orc.decode_bin_general(c["xy"][b], c["frozen"], c["r"])
         assert np.array_equal(i2, c["info"][b])
         assert np.array_equal(x2, c["xhat"][b])
+
+
+@pytest.mark.parametrize("idx", range(40))
+def test_edge_long_cases(idx):
+    """The oracle against the reference's decodes of the edge families at N = 1024 / 4096
+    (edge_long.npz), before the GPU tests trust it on them."""
+    c = edge_long_cases()[idx]
+    info, xhat = orc.decode_bin(c["xy"], c["frozen"], c["fval"])
+    assert np.array_equal(info, c["info"]), c["family_name"]
+    assert np.array_equal(xhat, c["xhat"]), c["family_name"]
 
 
 def test_nonuniform_prior_two_trees():

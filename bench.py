@@ -248,6 +248,8 @@ class Deletion:
         self.K = self.code.K
         if a.del_lanes:
             sc.set_deletion_lanes(a.del_lanes)
+        if a.del_rate1 >= 0:
+            sc.set_deletion_rate1(a.del_rate1)
         self.dec = sc.DeletionDecoder(self.code, self.n0, self.pd, self.ones)
         # Philox keyed by the global codeword index: rank r's shard is codewords [r*B, (r+1)*B) of
         # the one-GPU run, so sharded counters sum to the single run's
@@ -557,6 +559,8 @@ def build_parser():
     ap.add_argument("--ones", type=int, default=0, help="deletion: guard-band ones (numberOfOnesToAddAtBothEndsOfGuardbands)")
     ap.add_argument("--del-k", type=int, default=0, help="deletion: information bits (0 = the configuration's frozen set)")
     ap.add_argument("--del-lanes", type=int, default=0, help="deletion: lanes a codeword of the table-driven layout (0 = the library's)")
+    ap.add_argument("--del-rate1", type=int, default=-1,
+                    help="deletion: 0 = the 8-lane subtrees without the rate-1 shortcut (diagnostic A/B; -1 = the library's)")
     ap.add_argument("--pd", type=float, default=0.1, help="deletion probability")
     ap.add_argument("--xi", type=float, default=0.1, help="guard-band parameter")
     ap.add_argument("--q", type=int, default=4)

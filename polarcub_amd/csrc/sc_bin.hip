@@ -62,6 +62,7 @@ KernFn variant_kernel(int v) {
     if (KernFn k = bin_kernel_part1(v)) return k;
     if (KernFn k = bin_kernel_part2(v)) return k;
     if (KernFn k = bin_kernel_part4(v)) return k;
+    if (KernFn k = bin_kernel_part8(v)) return k;
     return bin_kernel_part5(v);
 }
 
@@ -156,10 +157,17 @@ bool fits(int v, int n) {
 }
 int pick_variant(int n) {
     if (fits(g_variant, n)) return g_variant;
-    // past the split level's LDS budget with the bits in LDS (N = 4096, 8192): the split level with
-    // the bits in scratch, one stored depth fewer (N = 4096 13.1 -> 14.1 M cw/s, N = 8192 5.2 -> 5.7 M;
-    // equal at N = 16384, where variant 17 stays)
-    if (n <= 13 && g_variant == kDefaultVariant && fits(31, n)) return 31;
+    // past the split level's LDS budget with the bits in LDS (N = 4096, 8192): the split level at G = 8
+    // lanes a codeword (a node of 512 positions: one stored depth fewer than G = 4), with its bits in
+    // LDS at N = 4096 (variant 30: 15.5 -> 17.8 M cw/s, 362 -> 314 KB/cw) and in the slot scratch at
+    // N = 8192 (33: 6.1 -> 6.6 M), round 6; before them the G = 4 split level with the bits in scratch
+    // (31: N = 4096 13.1 -> 14.1 M cw/s, N = 8192 5.2 -> 5.7 M over variant 24; equal at N = 16384,
+    // where variant 17 stays)
+    if (g_variant == kDefaultVariant) {
+        if (n == 12 && fits(30, n)) return 30;
+        if (n == 13 && fits(33, n)) return 33;
+        if (n <= 13 && fits(31, n)) return 31;
+    }
     constexpr int kFallback[] = {24, 17, 13, 14, 10, 0, 1};
     for (int v : kFallback)
         if (fits(v, n)) return v;
@@ -277,6 +285,7 @@ int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N
     BinKernFn kern = nullptr;
     if (g_experiment && tile == 64 / kVar[v].G) kern = exp_kernel(g_experiment, v, xc != nullptr);
     if (!kern && g_tiled_root && tile == 64 / kVar[v].G) kern = bin_kernel_tiled_root(v, xc != nullptr);
+    if (!kern && g_tiled_root && tile == 64 / kVar[v].G) kern = bin_kernel_tiled_root2(v, xc != nullptr);
     if (!kern) kern = xc ? bin_kernel_compact(v) : variant_kernel(v);
     if (!kern) return PCUB_EINVAL;
     hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(kBlock), launch_lds(v, log2N), st, A);

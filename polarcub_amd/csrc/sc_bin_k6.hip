@@ -9,6 +9,8 @@ BinKernFn bin_kernel_compact(int v) {
         case 24: return k_sc_bin<32, 4, 3, false, 1, true, false, 0, true>;
         case 26: return k_sc_bin<32, 4, 2, false, 1, true, true, 2, true>;
         case 31: return k_sc_bin<32, 4, 2, false, 1, false, true, 2, true>;
+        case 30: return k_sc_bin<32, 8, 2, false, 1, true, true, 2, true>;
+        case 33: return k_sc_bin<32, 8, 2, false, 1, false, true, 2, true>;
         default: return nullptr;
     }
 }

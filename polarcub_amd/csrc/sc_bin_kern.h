@@ -22,7 +22,7 @@ constexpr int kBinBlock = 256;
 struct Variant {
     int S, G, W, L, T, Y, H, P;
 };
-constexpr int kNumVariants = 33;
+constexpr int kNumVariants = 34;
 constexpr Variant kVar[kNumVariants] = {
     {16, 1, 2, 0, 0}, {8, 1, 4, 0, 0}, {32, 1, 1, 0, 0}, {16, 4, 2, 0, 0}, {8, 4, 4, 0, 0}, {16, 2, 2, 0, 0},
     {32, 2, 1, 0, 0}, {8, 8, 4, 0, 0}, {16, 2, 2, 0, 1}, {8, 8, 4, 0, 1}, {16, 4, 2, 0, 1}, {8, 4, 4, 1, 0},
@@ -32,6 +32,7 @@ constexpr Variant kVar[kNumVariants] = {
     {32, 4, 3, 0, 1, 1}, {32, 8, 3, 0, 1, 1},
     {32, 4, 2, 0, 1, 1, 1, 2}, {32, 4, 2, 0, 1, 1, 1, 1}, {32, 4, 2, 0, 1, 1, 1, 3}, {32, 4, 3, 0, 1, 1, 0, 2},
     {32, 8, 2, 0, 1, 1, 1, 2}, {32, 4, 2, 0, 1, 0, 1, 2}, {16, 8, 3, 0, 1, 1, 1, 2},
+    {32, 8, 2, 0, 1, 0, 1, 2},
 };
 
 // LDS bytes of the stage level (L: S pairs per thread) or of the split level's LDS half (H: S doubles)
@@ -81,10 +82,12 @@ BinKernFn bin_kernel_part1(int v);
 BinKernFn bin_kernel_part2(int v);
 BinKernFn bin_kernel_part4(int v);
 BinKernFn bin_kernel_part5(int v);
+BinKernFn bin_kernel_part8(int v);
 // the compact-root twin of variant v (CR: root rows as compact normalised doubles), or nullptr
 BinKernFn bin_kernel_compact(int v);
 // variant v reading its root in the wave's own tiles (TR: tile = 64 / G, a wave-uniform base and
 // 32-bit lane offsets), pairs or compact rows; nullptr where not instantiated (sc_bin_k7.hip)
 BinKernFn bin_kernel_tiled_root(int v, bool compact);
+BinKernFn bin_kernel_tiled_root2(int v, bool compact);  // sc_bin_k9.hip: the N >= 4096 variants' twins
 
 }  // namespace pcub

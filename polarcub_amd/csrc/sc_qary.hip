@@ -100,7 +100,8 @@ size_t qsym_lds_bytes(int n, int G, int q) {
 size_t qhl_lds_bytes(int q, int S) { return (size_t)kQBlock * S * q * sizeof(double); }
 // the HL kernels' launch bounds: three workgroups a CU (q = 4: 4 KB of 2-bit symbols + 32 KB of the
 // split level a workgroup would let four share the LDS, but the registers allow three)
-int q_hl_waves(int) { return 3; }
+// (S = 8, q = 4: 64 KB of split level a workgroup, two a CU)
+int q_hl_waves(int q, int S) { return q * S >= 32 ? 2 : 3; }
 
 QGeom q_geom(int q, int n) {
     QGeom c{4, g_qlanes, false, false};  // 8 register positions (q <= 4) via pcub_sc_set_qary_regs
@@ -118,13 +119,13 @@ QGeom q_geom(int q, int n) {
     // the split level (with the symbols in LDS) where its three workgroups fit a CU and the code
     // has an outer level above it (N >= 4 S G)
     c.hl = c.yl && g_qhl && qary_kernel_h(q, c.S, c.G) && (1 << n) >= 4 * c.S * c.G &&
-           (size_t)q_hl_waves(q) * (qsym_lds_bytes(n, c.G, q) + qhl_lds_bytes(q, c.S)) <= kQLdsPerCu;
+           (size_t)q_hl_waves(q, c.S) * (qsym_lds_bytes(n, c.G, q) + qhl_lds_bytes(q, c.S)) <= kQLdsPerCu;
     return c;
 }
 
 QKern qkernel(int q, int n, int* waves = nullptr) {
     const QGeom c = q_geom(q, n);
-    if (waves) *waves = c.hl ? q_hl_waves(q) : qary_waves(q, c.S, c.G);
+    if (waves) *waves = c.hl ? q_hl_waves(q, c.S) : qary_waves(q, c.S, c.G);
     if (c.hl) return qary_kernel_h(q, c.S, c.G);
     return c.yl ? qary_kernel_y(q, c.S, c.G) : qary_kernel(q, c.S, c.G);
 }

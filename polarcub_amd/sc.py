@@ -685,6 +685,17 @@ def leaf_deletion_supported(n, n0, ones=0):
     return bool(_lib.lib().pcub_sc_leaf_deletion_supported(int(n), int(n0), int(ones)))
 
 
+def set_deletion_rate1(on):
+    """Diagnostic: 0 runs the 8-lane deletion subtrees without the rate-1 shortcut where that twin is
+    built (pcub_sc_set_deletion_rate1, not part of the stable ABI); returns the previous setting.
+    Decisions are identical either way."""
+    import ctypes
+    f = _lib.lib().pcub_sc_set_deletion_rate1
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int32]
+    return int(f(int(on)))
+
+
 def set_deletion_lanes(g):
     """Lanes a codeword of the table-driven deletion layout: 8 (default), 16, or 4 (up to 64
     trellises; 8 beyond) (pcub_sc_set_deletion_lanes); returns the previous value.  Decisions are

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     H = ctypes.CDLL(build.HOST_LIB)  # host-only construction library (include/polarcub_construct.h)
     missing = [n for n in sorted(_declared("polarcub_construct.h")) if not hasattr(H, n)]
     assert not missing, missing
-    assert _lib.lib().pcub_abi_version() == _lib.ABI_VERSION == 3
+    assert _lib.lib().pcub_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_built_variants_are_the_launchable_ones():

@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 BIN_SETS = ["bsc_n64", "awgn_n1024", "awgn_n4096", "awgn_n256_lowsnr"]
 # the kernel variants the library builds (sc_bin_kern.h; the ones pick_variant can launch): 24 and 26
 # keep the re-encoded bits in LDS, 26 and 31 split their last level (LDS + registers)
-VARIANTS = [0, 1, 10, 13, 14, 17, 24, 26, 31]
+VARIANTS = [0, 1, 10, 13, 14, 17, 24, 26, 30, 31, 33]
 
 
 def _xy(g):
@@ -155,7 +155,7 @@ def test_decode_then_reencode_roundtrip_large(sc):
     assert torch.equal(dx, x)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 17, 24, 26, 31])
+@pytest.mark.parametrize("variant", [0, 1, 17, 24, 26, 30, 31, 33])
 def test_tiled_root_layout(sc, variant):
     """pcub_sc_decode_bin_tiled: the root rows in tiles of T codewords ([ceil(B/T), N, T, 2], the
     kernel's own wave width and others, ragged last tiles) decode exactly as the [N, B, 2] rows, for

@@ -302,7 +302,8 @@ def test_dense_staging_any_stride(sc, n0, n):
 @pytest.mark.parametrize("n0,n", [(2, 6), (2, 7), (2, 8), (3, 7), (3, 8), (3, 9)])
 def test_dense_layout_lanes(sc, n0, n):
     """The table-driven layout with 16, 8 (the default up to 64 trellises) and 4 lanes a codeword
-    (pcub_sc_set_deletion_lanes: four, three and two cross-lane subtree levels) decodes identically:
+    (pcub_sc_set_deletion_lanes: four, three and two cross-lane subtree levels), and 8 without the
+    rate-1 shortcut (pcub_sc_set_deletion_rate1), decodes identically:
     ragged batch, the n0 = 2 table built per workgroup and given, n0 = 3 with its table; and agrees
     with the oracle on a sample."""
     N = 1 << n
@@ -320,13 +321,15 @@ def test_dense_layout_lanes(sc, n0, n):
     for use_table in ((True, False) if n0 == 2 else (True,)):
         d = sc.DeletionDecoder(code, n0, pd, use_table=use_table)
         outs = []
-        for g in (16, 8, 4):
+        for g, r1 in ((16, 1), (8, 1), (4, 1), (8, 0)):
             prev = sc.set_deletion_lanes(g)
+            prev_r1 = sc.set_deletion_rate1(r1)  # 0: the 8-lane subtrees without the rate-1 shortcut
             try:
                 info, xhat = d.decode(rxt, ln)
                 torch.cuda.synchronize()
             finally:
                 sc.set_deletion_lanes(prev)
+                sc.set_deletion_rate1(prev_r1)
             outs.append((info.cpu().numpy(), xhat.cpu().numpy()))
         for o in outs[1:]:
             assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1]), use_table

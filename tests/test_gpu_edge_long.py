@@ -15,7 +15,7 @@ from tests.conftest import edge_cases, edge_long_cases
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 10, 13, 14, 17, 24, 26, 31]
+VARIANTS = [0, 1, 10, 13, 14, 17, 24, 26, 30, 31, 33]
 
 
 @pytest.fixture(scope="module")

@@ -160,12 +160,13 @@ int pick_variant(int n) {
     // past the split level's LDS budget with the bits in LDS (N = 4096, 8192): the split level at G = 8
     // lanes a codeword (a node of 512 positions: one stored depth fewer than G = 4), with its bits in
     // LDS at N = 4096 (variant 30: 15.5 -> 17.8 M cw/s, 362 -> 314 KB/cw) and in the slot scratch at
-    // N = 8192 (33: 6.1 -> 6.6 M), round 6; before them the G = 4 split level with the bits in scratch
-    // (31: N = 4096 13.1 -> 14.1 M cw/s, N = 8192 5.2 -> 5.7 M over variant 24; equal at N = 16384,
-    // where variant 17 stays)
+    // N = 8192, 16384 (33: 6.1 -> 6.6 M; 2.28 -> 2.68 M over 17), round 6; before them the G = 4 split
+    // level with the bits in scratch
+    // (31: N = 4096 13.1 -> 14.1 M cw/s, N = 8192 5.2 -> 5.7 M over variant 24; equal to 17 at
+    // N = 16384); N >= 32768 keeps variant 17 (not measured against 33)
     if (g_variant == kDefaultVariant) {
         if (n == 12 && fits(30, n)) return 30;
-        if (n == 13 && fits(33, n)) return 33;
+        if ((n == 13 || n == 14) && fits(33, n)) return 33;
         if (n <= 13 && fits(31, n)) return 31;
     }
     constexpr int kFallback[] = {24, 17, 13, 14, 10, 0, 1};

@@ -22,7 +22,6 @@ QKern qary_kernel_q4(int S, int G) {
 // the C4 geometry with its symbols in LDS (4 words of 2-bit symbols a thread at N = 256)
 QKern qary_kernel_q4_y(int S, int G) {
     if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, qary_waves(4, 4, 4), 1, true>;
-    if (S == 8 && G == 4) return k_sc_qary<4, 8, 4, qary_waves(4, 8, 4), 1, true>;
     return nullptr;
 }
 
@@ -31,16 +30,12 @@ QKern qary_kernel_q4_y(int S, int G) {
 // 128 of four workgroups it spilled 119 VGPRs and ran 2 % slower, 88.3 vs 90.0 M cw/s)
 QKern qary_kernel_q4_h(int S, int G) {
     if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 3, 1, true, true>;
-    // 2S = 16 positions a lane at the chain's end (8 in LDS: 64 KB a workgroup, two a CU): at N = 256 one
-    // stored stage depth instead of two (round 6, pcub_sc_set_qary_regs(8))
-    if (S == 8 && G == 4) return k_sc_qary<4, 8, 4, 2, 1, true, true>;
     return nullptr;
 }
 
 // ... reading its root rows in the wave's own tiles (TR: tile = 16, a wave-uniform base)
 QKern qary_kernel_q4_h_tr(int S, int G) {
     if (S == 4 && G == 4) return k_sc_qary<4, 4, 4, 3, 1, true, true, true>;
-    if (S == 8 && G == 4) return k_sc_qary<4, 8, 4, 2, 1, true, true, true>;
     return nullptr;
 }
 

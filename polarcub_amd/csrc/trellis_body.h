@@ -443,26 +443,54 @@ PCUB_HD void segment_of(const BitF& bit, int len, int levels, int t, int& s, int
 // The same parse on a bit-packed received word (bit i of word i >> 5 = symbol i == 1,
 // bits past the word's length 0): each probe covers 32 symbols, so a guard band of
 // zeros is crossed in a few LDS reads instead of one dependent byte load per symbol.
-// first symbol 1 in [a, e), or e
+// first symbol 1 in [a, e), or e.  The first word alone (at n = 8 a trim almost always finds its one
+// there); past it, four words a probe (independent loads, clamped to the range's words and masked), so
+// a longer guard band's zero run (n >= 10) costs one round trip per 128 symbols instead of one per
+// word (round 6: n = 10 85 -> 90 M cw/s; probing four words from the start cost C5 17 %).
 PCUB_HD int first_one(const uint32_t* w, int a, int e) {
-    while (a < e) {
-        const uint32_t x = w[a >> 5] >> (a & 31);
-        if (x) {
-            const int i = a + __builtin_ctz(x);
-            return i < e ? i : e;
-        }
-        a = (a | 31) + 1;
+    if (a >= e) return e;
+    int wi = a >> 5;
+    const uint32_t x = w[wi] >> (a & 31);
+    if (x) {
+        const int i = a + __builtin_ctz(x);
+        return i < e ? i : e;
+    }
+    const int last = (e - 1) >> 5;  // the last word the range touches
+    for (++wi; wi <= last; wi += 4) {
+        const int i1 = wi + 1 <= last ? wi + 1 : last, i2 = wi + 2 <= last ? wi + 2 : last,
+                  i3 = wi + 3 <= last ? wi + 3 : last;
+        const uint32_t x0 = w[wi];
+        const uint32_t x1 = wi + 1 <= last ? w[i1] : 0u;
+        const uint32_t x2 = wi + 2 <= last ? w[i2] : 0u;
+        const uint32_t x3 = wi + 3 <= last ? w[i3] : 0u;
+        const int i = x0   ? (wi << 5) + __builtin_ctz(x0)
+                      : x1 ? ((wi + 1) << 5) + __builtin_ctz(x1)
+                      : x2 ? ((wi + 2) << 5) + __builtin_ctz(x2)
+                      : x3 ? ((wi + 3) << 5) + __builtin_ctz(x3)
+                           : -1;
+        if (i >= 0) return i < e ? i : e;
     }
     return e;
 }
 
-// last symbol 1 in [a, e); one must exist
+// last symbol 1 in [a, e); one must exist (so the probes never pass word 0 without finding it)
 PCUB_HD int last_one(const uint32_t* w, int e) {
-    int b = e - 1;
-    for (;;) {
-        const uint32_t x = w[b >> 5] << (31 - (b & 31));
-        if (x) return b - __builtin_clz(x);
-        b = (b & ~31) - 1;
+    const int b = e - 1;
+    int wi = b >> 5;
+    const uint32_t x = w[wi] << (31 - (b & 31));
+    if (x) return b - __builtin_clz(x);
+    for (--wi;; wi -= 4) {
+        const int i1 = wi >= 1 ? wi - 1 : 0, i2 = wi >= 2 ? wi - 2 : 0, i3 = wi >= 3 ? wi - 3 : 0;
+        const uint32_t x0 = w[wi];
+        const uint32_t x1 = wi >= 1 ? w[i1] : 0u;
+        const uint32_t x2 = wi >= 2 ? w[i2] : 0u;
+        const uint32_t x3 = wi >= 3 ? w[i3] : 0u;
+        const int i = x0   ? (wi << 5) + 31 - __builtin_clz(x0)
+                      : x1 ? ((wi - 1) << 5) + 31 - __builtin_clz(x1)
+                      : x2 ? ((wi - 2) << 5) + 31 - __builtin_clz(x2)
+                      : x3 ? ((wi - 3) << 5) + 31 - __builtin_clz(x3)
+                           : -1;
+        if (i >= 0) return i;
     }
 }
 

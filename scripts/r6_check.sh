@@ -21,6 +21,12 @@ for rep in 1 2; do
   run c4_s4_$rep "--workload qary --steps 10 --warmup 3 --no-cpu --no-e2e" || exit 1
   run c4_s8_$rep "--workload qary --steps 10 --warmup 3 --no-cpu --no-e2e --qregs 8" || exit 1
 done
+for rep in 1 2; do
+  run c5_$rep "--workload deletion --steps 10 --warmup 3 --no-cpu" || exit 1
+  run c5k64_$rep "--workload deletion --del-k 64 --steps 10 --warmup 3 --no-cpu" || exit 1
+done
+run d10 "--workload deletion --n 10 --steps 5 --warmup 2 --no-cpu" || exit 1
 run n14_v17 "--n 14 --batch 131072 --steps 3 --warmup 1 --no-cpu --no-e2e" || exit 1
 run n14_v33 "--n 14 --batch 131072 --steps 3 --warmup 1 --no-cpu --no-e2e --variant 33" || exit 1
+WL=deletion TAG=${OUT:-r6chk}/del_n8_n02_dense EXTRA="" bash scripts/prof_sq.sh || exit 1
 exit 0

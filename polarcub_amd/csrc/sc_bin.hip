@@ -30,6 +30,13 @@ static BinKernFn exp_kernel(int e, int v, bool compact) {
     return pcub_exp_kernel ? (BinKernFn)pcub_exp_kernel(e, v, compact ? 1 : 0) : nullptr;
 }
 static std::atomic<int> g_experiment{0};
+// the q-ary decode's twin compiled for its code length (sc_qary_q4.hip) where one exists (diagnostic
+// A/B switch, not the ABI: pcub_sc_set_fixed_n(0) runs the generic kernels; identical outputs).  The
+// binary tiled-root twins specialised the same way (N = 1024, 4096) measured slower -- 100.8 -> 99.6 M
+// and 17.9 -> 16.1 M cw/s: SGPR spills 508 -> 20 but VGPR spills 50 -> 74 -- and were removed (round 6).
+static std::atomic<int> g_fixed_n{1};
+extern "C" int pcub_sc_set_fixed_n(int on) { return g_fixed_n.exchange(on ? 1 : 0); }
+extern "C" int pcub_sc_fixed_n(void) { return g_fixed_n.load(std::memory_order_relaxed); }
 extern "C" int pcub_sc_set_experiment(int e) {
     const int old = g_experiment.exchange(e);
     return old;

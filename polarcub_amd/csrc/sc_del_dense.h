@@ -73,14 +73,15 @@ PCUB_HD uint32_t packed_bits(const uint32_t* w, int s, int m, int rw) {
 template <int TB, int GB = 4>
 PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, int* se) {
     constexpr int TL = TB - GB;
+    constexpr bool P4 = TB >= 7;  // long guard bands (n >= 10): four-word probes (trellis_body.h)
     int a = 0, e = len;
-    trim_range_packed(pw, a, e);
+    trim_range_packed<P4>(pw, a, e);
 #pragma unroll
     for (int k = GB - 1; k >= 0; --k) {
         const int h = (e - a) / 2;
         if ((jr >> k) & 1u) a += h;
         else e = a + h;
-        trim_range_packed(pw, a, e);
+        trim_range_packed<P4>(pw, a, e);
     }
     sa[0] = a;
     se[0] = e;
@@ -90,8 +91,8 @@ PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, i
         for (int i = (1 << lev) - 1; i >= 0; --i) {
             const int a0 = sa[i], e0 = se[i], h = (e0 - a0) / 2;
             int la = a0, le = a0 + h, ra = a0 + h, re = e0;
-            trim_range_packed(pw, la, le);
-            trim_range_packed(pw, ra, re);
+            trim_range_packed<P4>(pw, la, le);
+            trim_range_packed<P4>(pw, ra, re);
             sa[2 * i] = la;
             se[2 * i] = le;
             sa[2 * i + 1] = ra;

@@ -72,6 +72,7 @@ __global__ __launch_bounds__(kQBlock) void k_encode_qary(const uint8_t* info, lo
 // kernel linked in as pcub_exp_qkernel, launched while pcub_sc_set_experiment selects it
 extern "C" __attribute__((weak)) void* pcub_exp_qkernel(int e, int q, int S, int G);
 extern "C" int pcub_sc_experiment(void);
+extern "C" int pcub_sc_fixed_n(void);  // sc_bin.hip: the code-length-specialised twins allowed
 
 int g_qlanes = 4;  // requested lanes per codeword (pcub_sc_set_qary_lanes)
 int g_qylds = 1;   // symbols in LDS where a twin kernel exists and fits (pcub_sc_set_qary_lds)
@@ -224,6 +225,8 @@ int decode_qary_impl(const double* xy, int64_t B, int32_t log2N, int32_t q, int3
     QKern kern = nullptr;
     if (pcub_exp_qkernel && pcub_sc_experiment() && c.hl && tile == 64 / c.G)
         kern = (QKern)pcub_exp_qkernel(pcub_sc_experiment(), q, c.S, c.G);
+    if (!kern && g_qtr && c.hl && tile == 64 / c.G && q == 4 && pcub_sc_fixed_n())
+        kern = qary_kernel_q4_h_tr_n(c.S, c.G, log2N);
     if (!kern && g_qtr && c.hl && tile == 64 / c.G) kern = qary_kernel_h_tr(q, c.S, c.G);
     if (!kern) kern = qkernel(q, log2N);
     hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(kQBlock), qlaunch_lds(q, log2N), st, A);

@@ -535,7 +535,10 @@ PCUB_HD void q_final_dispatch(const QPass& P, QV<Q>* v, bool gop, bool root, dou
 // HL: the chain ends at a split level of 2S positions per lane (the first S in the LDS column
 //     hl, the rest in registers; q_hl_run): one stored stage depth fewer (8qN bytes written and
 //     8qN read less per codeword)
-template <int Q, int S, int G = 1, int U = 1, bool YL = false, bool HL = false, bool TR = false>
+// NC >= 0: the code length 2^NC is a compile-time constant (the kernel runs only at it), so the per-
+// position row offsets and level bases fold (binary decode_codeword's NC); TR kernels also know
+// their tile width, 64 / G.
+template <int Q, int S, int G = 1, int U = 1, bool YL = false, bool HL = false, bool TR = false, int NC = -1>
 PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool store, int j = 0, int lane = 0,
                             uint32_t* ylds = nullptr, long long ystride = 0, double* hl = nullptr) {
     constexpr int SR = HL ? 2 * S : S;  // positions per lane at the chain's last level
@@ -545,7 +548,8 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
     constexpr int QP = (Q + 1) / 2;
     static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "lanes per codeword");
     static_assert(SU <= 64, "a register subtree's frozen bits fit one 64-bit word");
-    const int nv = A.n - g;
+    const int n = NC >= 0 ? NC : A.n;
+    const int nv = n - g;
     const int Nv = 1 << nv;
     const long long ns = A.nslots;
     const int D = nv - s;  // depth of the register nodes
@@ -554,17 +558,17 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
     const long long ys = YL ? ystride : ns;  // symbol word stride
     // root rows of lane j: real position j + G*t is row bitrev_n(j) + bitrev_{nv}(t)
     // tiled layout: codeword cw's row 0 at ((cw / T) N) T + cw % T, rows T apart
-    const long long rs = A.tile > 0 ? (long long)A.tile : A.B;
-    const long long rb = A.tile > 0 ? (cw / A.tile) * ((long long)A.tile << A.n) + cw % A.tile : cw;
+    const long long rs = TR ? 64 / G : A.tile > 0 ? (long long)A.tile : A.B;
+    const long long rb = A.tile > 0 ? (cw / rs) * (rs << n) + cw % rs : cw;
     // TR (tile = the wave's 64 / G codewords): the tile's base wave-uniform (SGPRs), this lane's rows
     // a 32-bit byte offset (binary decode_codeword's TR)
     const double* in;
     uint32_t lin = 0;
     if constexpr (TR) {
-        in = A.xy + uniform64((cw / A.tile) * ((long long)A.tile << A.n)) * Q;
-        lin = (uint32_t)((cw % A.tile + (long long)bitrev((uint32_t)j, A.n) * rs) * Q * 8);
+        in = A.xy + uniform64((cw / rs) * (rs << n)) * Q;
+        lin = (uint32_t)((cw % rs + (long long)bitrev((uint32_t)j, n) * rs) * Q * 8);
     } else {
-        in = A.xy + (rb + (long long)bitrev((uint32_t)j, A.n) * rs) * Q;
+        in = A.xy + (rb + (long long)bitrev((uint32_t)j, n) * rs) * Q;
     }
     QInfo qi{A.info, A.B, cw, store, 0, j, G - 1, 0u};
     for (int k = 0; k < (1 << D); ++k) {
@@ -668,7 +672,7 @@ PCUB_HD void decode_qary_cw(const QArgs& A, long long cw, long long slot, bool s
     // x_hat[i] is the root's half-split position bitrev(i): lane j holds the rows
     // bitrev_n(j) + bitrev_{nv}(t), t = its local position
     if (A.xhat && store) {
-        uint8_t* xo = A.xhat + cw + (long long)bitrev((uint32_t)j, A.n) * A.B;
+        uint8_t* xo = A.xhat + cw + (long long)bitrev((uint32_t)j, n) * A.B;
         for (int t = 0; t < Nv; ++t) xo[(long long)bitrev((uint32_t)t, nv) * A.B] = (uint8_t)q_sym<Q, YL>(Y, ys, t);
     }
 }

@@ -26,7 +26,7 @@ constexpr int qary_waves(int q, int S, int G = 4) {
 // YL: the re-encoded symbols in dynamic LDS ([Nv/4 words][kQaryBlock]) instead of the slot
 // HL: the split last level's LDS half after them ([S * Q doubles][kQaryBlock], decode_qary_cw)
 template <int Q, int S, int G, int W = qary_waves(Q, S, G), int U = 1, bool YL = false, bool HL = false,
-          bool TR = false>
+          bool TR = false, int NC = -1>
 __global__ __launch_bounds__(kQaryBlock, W) void k_sc_qary(QArgs A) {
     static_assert(kQaryBlock == kQHlStride, "split-level LDS column stride");
     extern __shared__ uint32_t qsym_lds[];
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(kQaryBlock, W) void k_sc_qary(QArgs A) {
     for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const long long cw = t * CWB + threadIdx.x / G;
         const bool valid = cw < A.B;
-        decode_qary_cw<Q, S, G, U, YL, HL, TR>(A, valid ? cw : A.B - 1, slot, valid, j, lane,
+        decode_qary_cw<Q, S, G, U, YL, HL, TR, NC>(A, valid ? cw : A.B - 1, slot, valid, j, lane,
                                            YL ? qsym_lds + threadIdx.x : nullptr, kQaryBlock, hl);
     }
 }
@@ -60,6 +60,8 @@ QKern qary_kernel_q4_h(int S, int G);
 inline QKern qary_kernel_h(int q, int S, int G) { return q == 4 ? qary_kernel_q4_h(S, G) : nullptr; }
 // the split-level kernel reading its root in the wave's own tiles (decode_qary_cw's TR), or nullptr
 QKern qary_kernel_q4_h_tr(int S, int G);
+// ... compiled for code length 2^n alone (NC = n; the C4 shape, n = 8), or nullptr
+QKern qary_kernel_q4_h_tr_n(int S, int G, int n);
 inline QKern qary_kernel_h_tr(int q, int S, int G) { return q == 4 ? qary_kernel_q4_h_tr(S, G) : nullptr; }
 inline QKern qary_kernel_y(int q, int S, int G) { return q == 4 ? qary_kernel_q4_y(S, G) : nullptr; }
 

@@ -39,4 +39,10 @@ QKern qary_kernel_q4_h_tr(int S, int G) {
     return nullptr;
 }
 
+// ... specialised on the C4 code length (N = 256): the per-position offsets fold (round 6)
+QKern qary_kernel_q4_h_tr_n(int S, int G, int n) {
+    if (S == 4 && G == 4 && n == 8) return k_sc_qary<4, 4, 4, 3, 1, true, true, true, 8>;
+    return nullptr;
+}
+
 }  // namespace pcub

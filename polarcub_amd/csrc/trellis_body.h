@@ -443,11 +443,35 @@ PCUB_HD void segment_of(const BitF& bit, int len, int levels, int t, int& s, int
 // The same parse on a bit-packed received word (bit i of word i >> 5 = symbol i == 1,
 // bits past the word's length 0): each probe covers 32 symbols, so a guard band of
 // zeros is crossed in a few LDS reads instead of one dependent byte load per symbol.
-// first symbol 1 in [a, e), or e.  The first word alone (at n = 8 a trim almost always finds its one
-// there); past it, four words a probe (independent loads, clamped to the range's words and masked), so
-// a longer guard band's zero run (n >= 10) costs one round trip per 128 symbols instead of one per
-// word (round 6: n = 10 85 -> 90 M cw/s; probing four words from the start cost C5 17 %).
+// first symbol 1 in [a, e), or e (a word a step)
 PCUB_HD int first_one(const uint32_t* w, int a, int e) {
+    while (a < e) {
+        const uint32_t x = w[a >> 5] >> (a & 31);
+        if (x) {
+            const int i = a + __builtin_ctz(x);
+            return i < e ? i : e;
+        }
+        a = (a | 31) + 1;
+    }
+    return e;
+}
+
+// last symbol 1 in [a, e); one must exist
+PCUB_HD int last_one(const uint32_t* w, int e) {
+    int b = e - 1;
+    for (;;) {
+        const uint32_t x = w[b >> 5] << (31 - (b & 31));
+        if (x) return b - __builtin_clz(x);
+        b = (b & ~31) - 1;
+    }
+}
+
+// The same scans for long guard bands (round 6): the first word alone, then four words a probe
+// (independent loads, clamped to the range's words and masked), so a zero run of up to ~100 symbols
+// past the first word costs one round trip instead of one per word.  The table-driven kernel uses them
+// from 128 trellises up (n = 10, 11: 85 -> 95 M cw/s at n = 10); at n = 8 (C5), where a trim nearly
+// always finds its one in the first word, the larger inlined scans cost 17 % and the plain ones stay.
+PCUB_HD int first_one_p4(const uint32_t* w, int a, int e) {
     if (a >= e) return e;
     int wi = a >> 5;
     const uint32_t x = w[wi] >> (a & 31);
@@ -473,8 +497,7 @@ PCUB_HD int first_one(const uint32_t* w, int a, int e) {
     return e;
 }
 
-// last symbol 1 in [a, e); one must exist (so the probes never pass word 0 without finding it)
-PCUB_HD int last_one(const uint32_t* w, int e) {
+PCUB_HD int last_one_p4(const uint32_t* w, int e) {
     const int b = e - 1;
     int wi = b >> 5;
     const uint32_t x = w[wi] << (31 - (b & 31));
@@ -494,13 +517,14 @@ PCUB_HD int last_one(const uint32_t* w, int e) {
     }
 }
 
+template <bool P4 = false>
 PCUB_HD void trim_range_packed(const uint32_t* w, int& s, int& e) {
-    const int a = first_one(w, s, e);
+    const int a = P4 ? first_one_p4(w, s, e) : first_one(w, s, e);
     if (a == e) {
         s = e = a;
         return;
     }
-    e = last_one(w, e) + 1;
+    e = (P4 ? last_one_p4(w, e) : last_one(w, e)) + 1;
     s = a;
 }
 

@@ -363,9 +363,9 @@ def test_run_bin_matches_pair_pipeline(code):
         assert torch.equal(torch.where(torch.signbit(xc), torch.ones_like(ab), ab), pairs[..., 1])
 
 
-@pytest.mark.parametrize("n", [5, 14])
+@pytest.mark.parametrize("n", [5, 15])
 def test_run_bin_without_a_compact_kernel(n):
-    """Code lengths whose variant has no compact-root twin (n <= 5, n >= 14): the pipeline
+    """Code lengths whose variant has no compact-root twin (n <= 5, n >= 15): the pipeline
     generates normalised pairs and decodes them with pcub_sc_decode_bin (no expansion buffer), and
     counts exactly what the pair pipeline does on the same rows."""
     from polarcub_amd import _lib, construction, mc, sc
@@ -374,7 +374,7 @@ def test_run_bin_without_a_compact_kernel(n):
     s2 = construction.awgn_sigma2(1.0, 0.5)
     fr = construction.bhattacharyya_frozen(n, N // 2, s2)
     c = sc.CodeSpec.from_frozen_set(N, set(np.nonzero(fr)[0].tolist()), 1, device="cuda")
-    B = 700 if n == 14 else 5000
+    B = 700 if n == 15 else 5000
     got = mc.run_bin(c, 45, 300, B, mc.CHANNEL_AWGN, s2, chunk=256)
     info, pairs = mc.philox_norm_batch(c, 45, 300, B, mc.CHANNEL_AWGN, s2, compact=False)
     iw, _, _ = sc.BinaryDecoder(c).decode_native(pairs)

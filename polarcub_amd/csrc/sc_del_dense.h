@@ -73,7 +73,9 @@ PCUB_HD uint32_t packed_bits(const uint32_t* w, int s, int m, int rw) {
 template <int TB, int GB = 4>
 PCUB_HD void dense_segments(const uint32_t* pw, int len, uint32_t jr, int* sa, int* se) {
     constexpr int TL = TB - GB;
-    constexpr bool P4 = TB >= 7;  // long guard bands (n >= 10): four-word probes (trellis_body.h)
+    // four-word probes (trellis_body.h) at 128 trellises (n = 10: 85 -> 95 M cw/s); at 256 (n = 11:
+    // 30.0 -> 29.1 M) and at 64 (C5: 1.02 -> 0.86 G) the plain scans are faster
+    constexpr bool P4 = TB == 7;
     int a = 0, e = len;
     trim_range_packed<P4>(pw, a, e);
 #pragma unroll

@@ -469,8 +469,8 @@ PCUB_HD int last_one(const uint32_t* w, int e) {
 // The same scans for long guard bands (round 6): the first word alone, then four words a probe
 // (independent loads, clamped to the range's words and masked), so a zero run of up to ~100 symbols
 // past the first word costs one round trip instead of one per word.  The table-driven kernel uses them
-// from 128 trellises up (n = 10, 11: 85 -> 95 M cw/s at n = 10); at n = 8 (C5), where a trim nearly
-// always finds its one in the first word, the larger inlined scans cost 17 % and the plain ones stay.
+// at 128 trellises (n = 10: 85 -> 95 M cw/s); at n = 8 (C5), where a trim nearly always finds its one
+// in the first word, the larger inlined scans cost 17 %, and at n = 11 3 %, so the plain ones stay.
 PCUB_HD int first_one_p4(const uint32_t* w, int a, int e) {
     if (a >= e) return e;
     int wi = a >> 5;

@@ -78,10 +78,11 @@ def test_invalid_arguments_are_rejected_without_touching_the_device():
     assert L.pcub_sc_deletion_dense_layout(10, 3, 0, 3000, ctypes.c_void_p(4096), 0.1) == 1  # header checked on device
     assert L.pcub_sc_deletion_dense_layout(12, 4, 0, 9000, None, 0.1) == 0
     assert L.pcub_sc_deletion_dense_layout(8, 2, 0, 30000, None, 0.1) == 0  # rows past the LDS budget
-    # the compact-root decode: a kernel of its own where the default variant has a twin (N = 1024,
-    # 4096), else an expansion into pairs (the Monte-Carlo pipeline then generates pairs itself)
+    # the compact-root decode: a kernel of its own where the default variant has a twin (N = 1024 ..
+    # 16384), else an expansion into pairs (the Monte-Carlo pipeline then generates pairs itself)
     assert L.pcub_sc_decode_bin_compact_direct(10) == 1 and L.pcub_sc_decode_bin_compact_direct(12) == 1
-    assert L.pcub_sc_decode_bin_compact_direct(14) == 0 and L.pcub_sc_decode_bin_compact_direct(5) == 0
+    assert L.pcub_sc_decode_bin_compact_direct(14) == 1
+    assert L.pcub_sc_decode_bin_compact_direct(15) == 0 and L.pcub_sc_decode_bin_compact_direct(5) == 0
     assert L.pcub_sc_decode_bin_compact_direct(30) == _lib.EINVAL
 
 

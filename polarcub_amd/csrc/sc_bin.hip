@@ -35,6 +35,10 @@ static std::atomic<int> g_experiment{0};
 // binary tiled-root twins specialised the same way (N = 1024, 4096) measured slower -- 100.8 -> 99.6 M
 // and 17.9 -> 16.1 M cw/s: SGPR spills 508 -> 20 but VGPR spills 50 -> 74 -- and were removed (round 6).
 static std::atomic<int> g_fixed_n{1};
+// k_sc_bin's wave tiles from a counter (BinArgs::wtiles) instead of a static stride (diagnostic A/B
+// switch, not the ABI: pcub_sc_set_dynamic_tiles(0) runs the static stride; identical outputs)
+static std::atomic<int> g_dyn_tiles{1};
+extern "C" int pcub_sc_set_dynamic_tiles(int on) { return g_dyn_tiles.exchange(on ? 1 : 0); }
 extern "C" int pcub_sc_set_fixed_n(int on) { return g_fixed_n.exchange(on ? 1 : 0); }
 extern "C" int pcub_sc_fixed_n(void) { return g_fixed_n.load(std::memory_order_relaxed); }
 extern "C" int pcub_sc_set_experiment(int e) {
@@ -51,10 +55,11 @@ constexpr int kBlock = kBinBlock;
 // rate-0 table: one byte per register subtree (first_frozen_depth); information-bit compress masks:
 // eight words per frozen-mask word (compress_masks)
 __global__ __launch_bounds__(kBlock) void k_ef_table(const uint32_t* fmask, int D, int SU, uint8_t* ef, int nwords,
-                                                     uint32_t* cmask) {
+                                                     uint32_t* cmask, unsigned long long* wtiles) {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     if (k < (1 << D)) ef[k] = (uint8_t)first_frozen_depth(fmask, k, D, SU);
     if (k < nwords) compress_masks(fmask[k], cmask + 8 * k);
+    if (k == 0) *wtiles = 0;  // the decode's wave-tile counter (BinArgs::wtiles), before the decode on the stream
 }
 
 template <int NN>
@@ -130,7 +135,8 @@ int tree_depth(int n, int v) {
 }
 size_t ef_only_bytes(int n, int v) { return (((size_t)1 << tree_depth(n, v)) + 255) & ~(size_t)255; }
 size_t cmask_words(int n) { return n >= 5 ? ((size_t)1 << n) / 32 : 1; }
-size_t ef_bytes(int n, int v) { return ef_only_bytes(n, v) + ((cmask_words(n) * 32 + 255) & ~(size_t)255); }
+// + 256 bytes for the wave-tile counter at the end of the table area
+size_t ef_bytes(int n, int v) { return ef_only_bytes(n, v) + ((cmask_words(n) * 32 + 255) & ~(size_t)255) + 256; }
 
 // per-slot bytes: virtual levels 1..D-1 (Nv/2 - S pairs) + Nv local encoding bits (unless in LDS)
 size_t slot_bytes(int n, int v) {
@@ -282,8 +288,10 @@ int decode_bin_impl(const double* xy, const double* xc, int64_t B, int32_t log2N
     char* slots = (char*)workspace + efb;
     const int nw = (int)cmask_words(log2N);
     const int eft = (1 << D) > nw ? (1 << D) : nw;
+    unsigned long long* wtiles = (unsigned long long*)((char*)workspace + efb - 256);
     hipLaunchKernelGGL(k_ef_table, dim3((unsigned)((eft + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, frozen_mask,
-                       D, bin_sr(v) * kVar[v].G, ef, nw, cmask);
+                       D, bin_sr(v) * kVar[v].G, ef, nw, cmask, wtiles);
+    A.wtiles = g_dyn_tiles.load(std::memory_order_relaxed) ? wtiles : nullptr;
     A.ef = ef;
     A.cmask = cmask;
     A.nslots = nslots;

@@ -48,6 +48,9 @@ struct BinArgs {
     const uint8_t* ef;         // [2^D] first rate-0 depth of each subtree's chain (first_frozen_depth)
     int tile;                  // root layout: 0 = [N][B] rows; T > 0 = [ceil(B/T)][N][T] (T codewords a tile)
     const uint32_t* cmask;     // [N/32][8] per frozen-mask word: compress masks mv0..mv4, info count, info mask
+    // k_sc_bin's wave tiles (64 / G codewords each) handed out by a counter (zeroed before the launch)
+    // instead of a static stride, so the waves finish together (round 6); null: the static stride
+    unsigned long long* wtiles = nullptr;
 };
 
 // Information-bit compress masks of one 32-bit frozen-mask word (Hacker's Delight 7-4, "compress"):

@@ -49,6 +49,14 @@ inline size_t bin_ylds_bytes(int v, int n) {
     return kVar[v].Y ? (size_t)kBinBlock * (((size_t)1 << n) / kVar[v].G / 32) * sizeof(uint32_t) : 0;
 }
 
+// the next wave tile of the launch's counter: one vector atomic from lane 0, its value made wave-uniform
+__device__ __forceinline__ long long next_wave_tile(unsigned long long* c, int lane) {
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(c, 1ull);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 0), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 0);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
 template <int S, int G, int W, bool LDS, int NT, bool YL = false, bool HL = false, int PF = 0, bool CR = false,
           bool TR = false>
 __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
@@ -61,13 +69,21 @@ __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {
     const int j = threadIdx.x & (G - 1);
     const int lane = threadIdx.x & 63;
     const Lvl last = LDS ? Lvl{lds_last + threadIdx.x, kBinBlock} : Lvl{nullptr, 0};
-    const long long ntiles = (A.B + CWB - 1) / CWB;
-    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const long long cw = t * CWB + threadIdx.x / G;
+    // wave tiles: a wave decodes 64 / G codewords at a time (its lanes' codewords are independent of the
+    // other waves', whose LDS columns are their own), either the static stride of the workgroup tiles
+    // (wave wv of workgroup b takes wave tiles (b + i * grid) * WPB + wv) or the next tile of a counter
+    constexpr int WPB = kBinBlock / 64, CWW = 64 / G;
+    static_assert(CWB == WPB * CWW, "workgroup tile = its waves' tiles");
+    const long long nwt = (A.B + CWW - 1) / CWW;
+    const int wv = threadIdx.x >> 6;
+    long long wt = A.wtiles ? next_wave_tile(A.wtiles, lane) : (long long)blockIdx.x * WPB + wv;
+    while (wt < nwt) {
+        const long long cw = wt * CWW + lane / G;
         const bool valid = cw < A.B;
         decode_codeword<S, G, LDS, NT, YL, HL, PF, CR, -1, TR>(A, valid ? cw : A.B - 1, j, lane, slot, valid, last,
                                                YL ? (uint32_t*)(lds_last + LDS2) + threadIdx.x : nullptr, kBinBlock,
                                                HL ? (double*)lds_last + threadIdx.x : nullptr);
+        wt = A.wtiles ? next_wave_tile(A.wtiles, lane) : wt + (long long)gridDim.x * WPB;
     }
 }
 

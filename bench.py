@@ -574,6 +574,8 @@ def build_parser():
     ap.add_argument("--max-blocks", type=int, default=0, help="cap decode workgroups per CU (0 = occupancy)")
     ap.add_argument("--seed", type=int, default=20250204)
     ap.add_argument("--master-port", type=int, default=0, help="rendezvous port when launching ranks (0 = free port)")
+    ap.add_argument("--static-tiles", action="store_true",
+                    help="decode kernels stride over their tiles statically instead of taking them from a counter (A/B)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-xhat", action="store_true")
     ap.add_argument("--no-tile", action="store_true", help="awgn: root rows [N][B][2] instead of the kernel's tiles")
@@ -603,6 +605,8 @@ def main(argv=None):
         shared = world > 1 and int(os.environ.get("LOCAL_WORLD_SIZE", world)) > ndev  # same on every rank
         device = torch.device("cuda", (local % max(1, ndev)) if world > 1 else 0)
         torch.cuda.set_device(device)
+        if a.static_tiles:
+            sc.set_dynamic_tiles(0)
         if world > 1 and not shared:
             dist.init_process_group("nccl", device_id=device)
         elif world > 1:

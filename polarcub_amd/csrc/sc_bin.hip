@@ -35,10 +35,12 @@ static std::atomic<int> g_experiment{0};
 // binary tiled-root twins specialised the same way (N = 1024, 4096) measured slower -- 100.8 -> 99.6 M
 // and 17.9 -> 16.1 M cw/s: SGPR spills 508 -> 20 but VGPR spills 50 -> 74 -- and were removed (round 6).
 static std::atomic<int> g_fixed_n{1};
-// k_sc_bin's wave tiles from a counter (BinArgs::wtiles) instead of a static stride (diagnostic A/B
-// switch, not the ABI: pcub_sc_set_dynamic_tiles(0) runs the static stride; identical outputs)
+// the decode kernels' work tiles from a counter (BinArgs / QArgs / DelArgs::wtiles) instead of a static
+// stride (diagnostic A/B switch, not the ABI: pcub_sc_set_dynamic_tiles(0) runs the static stride;
+// identical outputs).  C2 98.5 -> 109.7 M cw/s, N = 4096 17.6 -> 18.9 M (round 6).
 static std::atomic<int> g_dyn_tiles{1};
 extern "C" int pcub_sc_set_dynamic_tiles(int on) { return g_dyn_tiles.exchange(on ? 1 : 0); }
+extern "C" int pcub_sc_dynamic_tiles(void) { return g_dyn_tiles.load(std::memory_order_relaxed); }
 extern "C" int pcub_sc_set_fixed_n(int on) { return g_fixed_n.exchange(on ? 1 : 0); }
 extern "C" int pcub_sc_fixed_n(void) { return g_fixed_n.load(std::memory_order_relaxed); }
 extern "C" int pcub_sc_set_experiment(int e) {

@@ -53,6 +53,18 @@ struct BinArgs {
     unsigned long long* wtiles = nullptr;
 };
 
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+// The next work tile of a launch's counter (the decode kernels' dynamic tiles, round 6): one vector
+// atomic from lane 0, its value made wave-uniform
+__device__ __forceinline__ long long next_wave_tile(unsigned long long* c, int lane) {
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(c, 1ull);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 0), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 0);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+#endif
+
 // Information-bit compress masks of one 32-bit frozen-mask word (Hacker's Delight 7-4, "compress"):
 // with m = ~fm the information positions, x -> the bits of x at m packed to the right is
 //     x &= m;  for i in 0..4: t = x & mv_i;  x = (x ^ t) | (t >> 2^i)

@@ -49,14 +49,6 @@ inline size_t bin_ylds_bytes(int v, int n) {
     return kVar[v].Y ? (size_t)kBinBlock * (((size_t)1 << n) / kVar[v].G / 32) * sizeof(uint32_t) : 0;
 }
 
-// the next wave tile of the launch's counter: one vector atomic from lane 0, its value made wave-uniform
-__device__ __forceinline__ long long next_wave_tile(unsigned long long* c, int lane) {
-    unsigned long long v = 0;
-    if (lane == 0) v = atomicAdd(c, 1ull);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 0), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 0);
-    return (long long)(((unsigned long long)hi << 32) | lo);
-}
-
 template <int S, int G, int W, bool LDS, int NT, bool YL = false, bool HL = false, int PF = 0, bool CR = false,
           bool TR = false>
 __global__ __launch_bounds__(kBinBlock, W) void k_sc_bin(BinArgs A) {

@@ -20,6 +20,8 @@
 
 using namespace pcub;
 
+extern "C" int pcub_sc_dynamic_tiles(void);  // sc_bin.hip: work tiles from a counter
+
 namespace {
 
 constexpr int kMaxOnes = 3;
@@ -44,6 +46,29 @@ constexpr int kMaxDevices = 64;
 std::mutex g_gate_mu;
 unsigned long long* g_gate_ring[kMaxDevices] = {};
 std::atomic<unsigned long long> g_gate_next{1};
+
+// Per-launch group counters of the table-driven kernel (DelArgs::wtiles): a per-device ring, a slot a
+// launch, zeroed on the launch's stream before it (kGateRing launches in flight before a slot is reused).
+std::mutex g_ctr_mu;
+unsigned long long* g_ctr_ring[kMaxDevices] = {};
+std::atomic<unsigned long long> g_ctr_next{0};
+
+int counter_slot(unsigned long long** slot, hipStream_t st) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    if (dev < 0 || dev >= kMaxDevices) return (int)hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> lk(g_ctr_mu);
+        if (!g_ctr_ring[dev]) {
+            void* p = nullptr;
+            if ((e = hipMalloc(&p, kGateRing * sizeof(unsigned long long))) != hipSuccess) return (int)e;
+            g_ctr_ring[dev] = (unsigned long long*)p;
+        }
+    }
+    *slot = g_ctr_ring[dev] + (g_ctr_next.fetch_add(1) % kGateRing);
+    return (int)hipMemsetAsync(*slot, 0, sizeof(unsigned long long), st);
+}
 
 int gate_slot(unsigned long long** slot, unsigned long long* id) {
     int dev = 0;
@@ -216,6 +241,10 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     // segment-state table, so the launch is persistent
     if (dense || (n0 == 2 && ones == 0)) grid = resident_grid(k, lds, grid);
     if (grid * blk > 0xffffffffLL) return PCUB_EINVAL;  // 32-bit dispatch grid (work-items)
+    if (dense && pcub_sc_dynamic_tiles()) {
+        const int rc = counter_slot(&A.wtiles, (hipStream_t)stream);
+        if (rc) return rc;
+    }
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(blk), lds, (hipStream_t)stream, A);
     int rc = (int)hipGetLastError();
     if (rc || !checked) return rc;
@@ -223,6 +252,7 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     // the status word and leave when the table-driven launch succeeded)
     DelArgs F = A;
     F.tab = nullptr;
+    F.wtiles = nullptr;  // the gated fallback keeps the static stride
     const bool fb_dense = n0 == 2;
     const DelKern fk = fb_dense ? del_kernel_dense(2, n - n0, false, dg) : kern;
     const long long fcpb = fb_dense ? kDelBlock / dg : kDelBlock >> (n - n0);

@@ -240,8 +240,17 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
     const int g = threadIdx.x / G;
     const uint32_t jr = bitrev((uint32_t)j, GB);
     const long long ngrp = (A.B + CPB - 1) / CPB;
+    // codeword groups: the static stride, or the next group of the launch's counter (one atomic a group
+    // by thread 0, broadcast through LDS), so the workgroups finish together (round 6)
+    __shared__ long long next_grp;
+    long long grp = blockIdx.x;
+    if (A.wtiles) {
+        if (threadIdx.x == 0) next_grp = (long long)atomicAdd(A.wtiles, 1ull);
+        __syncthreads();
+        grp = next_grp;
+    }
 #pragma unroll 1
-    for (long long grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+    while (grp < ngrp) {
         const long long cw = grp * CPB + g;
         const bool valid = cw < A.B;
         const long long c = valid ? cw : A.B - 1;  // padding codewords decode a duplicate, store nothing
@@ -342,6 +351,13 @@ __global__ __launch_bounds__(kDelBlock, dense_waves(TB)) void k_sc_del_dense(Del
         if (A.xhat && valid)
             for (int i = j; i < WPC; i += G) A.xhat[(long long)i * A.B + cw] = xs[g * WPC + i];
         __syncthreads();  // xs / rxb are reused by the workgroup's next group
+        if (A.wtiles) {  // (every thread read next_grp before this group's first barrier)
+            if (threadIdx.x == 0) next_grp = (long long)atomicAdd(A.wtiles, 1ull);
+            __syncthreads();
+            grp = next_grp;
+        } else {
+            grp += gridDim.x;
+        }
     }
 }
 

@@ -68,6 +68,7 @@ struct DelArgs {
     const double* tab;      // n0 = 2, 3 without ones: the segment-state table (pcub_sc_deletion_build_table), or null
     unsigned long long* gate;     // null, or this launch's status word (a table the kernel rejected, sc_del.hip)
     unsigned long long gate_id;   // the value that marks the status word: this launch's table was rejected
+    unsigned long long* wtiles = nullptr;  // k_sc_del_dense: codeword groups from this counter (zeroed per launch)
 };
 
 // Segment-state tables (n0 = 2 and 3, pcub_sc_deletion_build_table) start with a header that every

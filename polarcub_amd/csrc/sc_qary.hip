@@ -35,9 +35,11 @@ __global__ __launch_bounds__(kQBlock) void k_q_frozen_words(const uint8_t* froze
     words[w] = o;
 }
 
-__global__ __launch_bounds__(kQBlock) void k_q_ef(const uint32_t* words, int D, int S, uint8_t* ef) {
+__global__ __launch_bounds__(kQBlock) void k_q_ef(const uint32_t* words, int D, int S, uint8_t* ef,
+                                                unsigned long long* wtiles) {
     const int k = blockIdx.x * kQBlock + threadIdx.x;
     if (k < (1 << D)) ef[k] = (uint8_t)first_frozen_depth(words, k, D, S);
+    if (k == 0) *wtiles = 0;  // the decode's wave-tile counter (QArgs::wtiles), before it on the stream
 }
 
 // q-ary encoder: u (info symbols at information positions, 0 at frozen ones)
@@ -73,6 +75,7 @@ __global__ __launch_bounds__(kQBlock) void k_encode_qary(const uint8_t* info, lo
 extern "C" __attribute__((weak)) void* pcub_exp_qkernel(int e, int q, int S, int G);
 extern "C" int pcub_sc_experiment(void);
 extern "C" int pcub_sc_fixed_n(void);  // sc_bin.hip: the code-length-specialised twins allowed
+extern "C" int pcub_sc_dynamic_tiles(void);  // sc_bin.hip: wave tiles from a counter
 
 int g_qlanes = 4;  // requested lanes per codeword (pcub_sc_set_qary_lanes)
 int g_qylds = 1;   // symbols in LDS where a twin kernel exists and fits (pcub_sc_set_qary_lds)
@@ -171,10 +174,10 @@ int q_depth(int n, int q) {
     return n - __builtin_ctz((unsigned)(c.sr() * c.G));
 }
 
-// rate-0 table + packed frozen words, ahead of the slots
+// rate-0 table + packed frozen words, ahead of the slots, and 256 bytes for the wave-tile counter
 size_t qtable_bytes(int n, int q) {
     const int D = q_depth(n, q);
-    return ((((size_t)1 << n) + 31) / 32 * 4 + ((size_t)1 << D) + 255) & ~(size_t)255;
+    return (((((size_t)1 << n) + 31) / 32 * 4 + ((size_t)1 << D) + 255) & ~(size_t)255) + 256;
 }
 
 }  // namespace
@@ -205,8 +208,9 @@ int decode_qary_impl(const double* xy, int64_t B, int32_t log2N, int32_t q, int3
     uint8_t* ef = (uint8_t*)workspace + ((size_t)N + 31) / 32 * 4;
     hipLaunchKernelGGL(k_q_frozen_words, dim3((unsigned)(((N + 31) / 32 + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0, st,
                        frozen, N, words);
+    unsigned long long* wtiles = (unsigned long long*)((char*)workspace + tb - 256);
     hipLaunchKernelGGL(k_q_ef, dim3((unsigned)(((1 << D) + kQBlock - 1) / kQBlock)), dim3(kQBlock), 0, st, words, D,
-                       c.sr() * c.G, ef);
+                       c.sr() * c.G, ef, wtiles);
     QArgs A;
     A.xy = xy;
     A.B = B;
@@ -218,6 +222,7 @@ int decode_qary_impl(const double* xy, int64_t B, int32_t log2N, int32_t q, int3
     A.nslots = g * kQBlock;
     A.ylds_words = c.yl ? (int)(qsym_lds_bytes(log2N, c.G, q) / kQBlock / sizeof(uint32_t)) : 0;
     A.tile = tile;
+    A.wtiles = pcub_sc_dynamic_tiles() ? wtiles : nullptr;
     char* slots = (char*)workspace + tb;
     A.scratch = (double2*)slots;
     A.ysym = c.yl ? nullptr : (uint32_t*)(slots + (size_t)A.nslots * (N / c.G - 2 * c.sr()) * ((q + 1) / 2) * sizeof(double2));

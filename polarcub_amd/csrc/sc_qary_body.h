@@ -165,6 +165,7 @@ struct QArgs {
     long long nslots;
     int ylds_words;          // symbol words per thread in LDS (YL kernels; the HL column follows them)
     int tile;                // root layout: 0 = [N][B][Q]; T > 0 = [ceil(B/T)][N][T][Q] (T codewords a tile)
+    unsigned long long* wtiles = nullptr;  // wave tiles from this counter (zeroed per launch), or the static stride
 };
 
 // Re-encoded symbols packed into 32-bit words: q = 4 in 2-bit fields (16 a word: the C4 kernel's

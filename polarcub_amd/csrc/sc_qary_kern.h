@@ -31,16 +31,20 @@ __global__ __launch_bounds__(kQaryBlock, W) void k_sc_qary(QArgs A) {
     static_assert(kQaryBlock == kQHlStride, "split-level LDS column stride");
     extern __shared__ uint32_t qsym_lds[];
     double* hl = HL ? (double*)(qsym_lds + A.ylds_words * kQaryBlock) + threadIdx.x : nullptr;
-    constexpr int CWB = kQaryBlock / G;  // codewords per tile
     const long long slot = (long long)blockIdx.x * kQaryBlock + threadIdx.x;
     const int j = threadIdx.x & (G - 1);
     const int lane = threadIdx.x & 63;
-    const long long ntiles = (A.B + CWB - 1) / CWB;
-    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const long long cw = t * CWB + threadIdx.x / G;
+    // wave tiles of 64 / G codewords (k_sc_bin's): the static stride of the workgroup tiles, or the
+    // next tile of the launch's counter so the waves finish together (round 6)
+    constexpr int WPB = kQaryBlock / 64, CWW = 64 / G;
+    const long long nwt = (A.B + CWW - 1) / CWW;
+    long long wt = A.wtiles ? next_wave_tile(A.wtiles, lane) : (long long)blockIdx.x * WPB + (threadIdx.x >> 6);
+    while (wt < nwt) {
+        const long long cw = wt * CWW + lane / G;
         const bool valid = cw < A.B;
         decode_qary_cw<Q, S, G, U, YL, HL, TR, NC>(A, valid ? cw : A.B - 1, slot, valid, j, lane,
                                            YL ? qsym_lds + threadIdx.x : nullptr, kQaryBlock, hl);
+        wt = A.wtiles ? next_wave_tile(A.wtiles, lane) : wt + (long long)gridDim.x * WPB;
     }
 }
 

@@ -696,6 +696,17 @@ def set_deletion_rate1(on):
     return int(f(int(on)))
 
 
+def set_dynamic_tiles(on):
+    """Diagnostic: 0 makes the binary, q-ary and deletion decode kernels stride over their tiles
+    statically instead of taking them from a per-launch counter (pcub_sc_set_dynamic_tiles, not part of
+    the stable ABI); returns the previous setting.  Decisions are identical either way."""
+    import ctypes
+    f = _lib.lib().pcub_sc_set_dynamic_tiles
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int]
+    return int(f(int(on)))
+
+
 def set_deletion_lanes(g):
     """Lanes a codeword of the table-driven deletion layout: 8 (default), 16, or 4 (up to 64
     trellises; 8 beyond) (pcub_sc_set_deletion_lanes); returns the previous value.  Decisions are

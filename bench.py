@@ -250,6 +250,8 @@ class Deletion:
             sc.set_deletion_lanes(a.del_lanes)
         if a.del_rate1 >= 0:
             sc.set_deletion_rate1(a.del_rate1)
+        if a.del_wave >= 0:
+            sc.set_deletion_wave(a.del_wave)
         self.dec = sc.DeletionDecoder(self.code, self.n0, self.pd, self.ones)
         # Philox keyed by the global codeword index: rank r's shard is codewords [r*B, (r+1)*B) of
         # the one-GPU run, so sharded counters sum to the single run's
@@ -259,6 +261,10 @@ class Deletion:
         self.outs = None
         self.dense = self.dec.dense_layout(self.rx.shape[1], self.rx.device)
         self.kernel = "k_sc_del_dense" if self.dense else "k_sc_del"
+        # n0 = 4, 64 .. 1024 trellises, no ones: the wave-per-task kernel (sc_del.hip's dispatch)
+        if (self.n0 == 4 and self.ones == 0 and 6 <= self.n - self.n0 <= 10 and a.del_wave != 0
+                and (self.rx.shape[1] + 31) // 32 * 4 <= 32768):
+            self.kernel = "k_sc_del_w4"
 
     def step(self):
         self.outs = self.dec.decode_native(self.rx, self.rx_len)
@@ -561,6 +567,8 @@ def build_parser():
     ap.add_argument("--del-lanes", type=int, default=0, help="deletion: lanes a codeword of the table-driven layout (0 = the library's)")
     ap.add_argument("--del-rate1", type=int, default=-1,
                     help="deletion: 0 = the 8-lane subtrees without the rate-1 shortcut (diagnostic A/B; -1 = the library's)")
+    ap.add_argument("--del-wave", type=int, default=-1,
+                    help="deletion n0 = 4: 0 = the lane-per-trellis kernel instead of the wave-per-task one (A/B; -1 = the library's)")
     ap.add_argument("--pd", type=float, default=0.1, help="deletion probability")
     ap.add_argument("--xi", type=float, default=0.1, help="guard-band parameter")
     ap.add_argument("--q", type=int, default=4)

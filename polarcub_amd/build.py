@@ -26,7 +26,7 @@ LIB = os.path.join(LIBDIR, "libpolarcub_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PCUB_ARCH", "gfx950")
 
-SOURCES = ["sc_del_dense.hip", "sc_del_n4w.hip", "sc_del_n4.hip", "sc_del_n4o.hip", "sc_del_n4x.hip", "sc_del_n3.hip", "sc_del_n3o.hip", "sc_del_n3x.hip",
+SOURCES = ["sc_del_w4.hip", "sc_del_dense.hip", "sc_del_n4w.hip", "sc_del_n4.hip", "sc_del_n4o.hip", "sc_del_n4x.hip", "sc_del_n3.hip", "sc_del_n3o.hip", "sc_del_n3x.hip",
            "sc_del_n2.hip", "sc_del_n2o.hip", "sc_del_n2x.hip", "sc_del_n1.hip", "sc_del_n1o.hip", "sc_del_n1x.hip",
            "sc_bin.hip", "sc_bin_k0.hip", "sc_bin_k1.hip", "sc_bin_k2.hip", "sc_bin_k4.hip", "sc_bin_k5.hip", "sc_bin_k6.hip", "sc_bin_k7.hip", "sc_bin_k8.hip", "sc_bin_k9.hip", "sc_qary.hip",
            "sc_qary_q2.hip", "sc_qary_q3.hip", "sc_qary_q4.hip", "sc_qary_q56.hip", "sc_qary_q78.hip",

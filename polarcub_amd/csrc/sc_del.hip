@@ -32,6 +32,9 @@ constexpr int kMaxStride = 1 << 24;
 std::atomic<int> g_dense{1};  // the table-driven layout allowed (pcub_sc_set_deletion_dense)
 std::atomic<int> g_dense_rate1{1};  // the 8-lane layout's rate-1 shortcut (pcub_sc_set_deletion_rate1)
 std::atomic<int> g_dense_lanes{8};  // lanes a codeword of the table-driven layout (8, 16; 4 up to 64 trellises)
+std::atomic<int> g_wave4{1};        // n0 = 4: the wave-per-task kernel allowed (pcub_sc_set_deletion_wave)
+// the wave-per-task kernel keeps its codeword's received word bit-packed in LDS next to ~80 KB of its own
+constexpr long long kW4MaxRxLds = 32768;
 
 // Status words of table-checked launches (one ring per device; sc_del_kern.h, DelArgs::gate): a
 // table-driven launch that rejects its table writes its launch id into its word, and the gated
@@ -211,6 +214,22 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     A.gate = nullptr;
     A.gate_id = 0;
     const long long rw = ((long long)stride + 31) / 32;
+    // n0 = 4 without ones (main_deletion's n = 12 .. 14): one wave a (trellis, depth-3 node) task, the
+    // trellises in LDS (sc_del_w4.hip), codewords from a per-launch counter
+    if (!exp && n0 == 4 && ones == 0 && g_wave4.load(std::memory_order_relaxed) && rw * 4 <= kW4MaxRxLds) {
+        const DelKern wk = del_kernel_w4(n - n0);
+        if (wk) {
+            A.rw = (int)rw;
+            const size_t lds = (size_t)(rw * 4);
+            const long long grid = resident_grid(wk, lds, B);
+            if (pcub_sc_dynamic_tiles()) {
+                const int rc = counter_slot(&A.wtiles, (hipStream_t)stream);
+                if (rc) return rc;
+            }
+            hipLaunchKernelGGL(wk, dim3((unsigned)grid), dim3(kDelBlock), lds, (hipStream_t)stream, A);
+            return (int)hipGetLastError();
+        }
+    }
     const bool dense = !exp && use_dense(n, n0, ones, stride, table);
     // the table-driven kernel checks the caller's table on the device (n0 = 3, and n0 = 2 with a table
     // given); behind it on the stream goes a gated fallback that decodes only if the check failed:
@@ -321,6 +340,11 @@ extern "C" int pcub_sc_set_deletion_lanes(int32_t g) {
 // the rate-1 shortcut where such a twin is built (n0 = 2 with a table, 64 / 256 trellises); the A/B
 // of DESIGN 3.2.  Decisions are identical either way.  Returns the previous setting.
 extern "C" int pcub_sc_set_deletion_rate1(int32_t on) { return g_dense_rate1.exchange(on ? 1 : 0); }
+
+// Diagnostic (not part of the stable ABI): 0 sends n0 = 4 decodes back to the lane-per-trellis kernel
+// k_sc_del instead of the wave-per-task kernel (sc_del_w4.hip); the A/B of DESIGN 3.2.  Decisions are
+// identical either way.  Returns the previous setting.
+extern "C" int pcub_sc_set_deletion_wave(int32_t on) { return g_wave4.exchange(on ? 1 : 0); }
 
 extern "C" int pcub_sc_set_deletion_dense(int32_t on) {
     return g_dense.exchange(on ? 1 : 0);

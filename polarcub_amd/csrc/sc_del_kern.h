@@ -755,6 +755,9 @@ PCUB_DEL_TABLE(4)
 // 512 and 1024 trellises of 2^4 inputs (a workgroup of T threads per codeword; main_deletion's
 // n0 = n // 3 at n = 13, 14), decode without ones: sc_del_n4w.hip
 DelKern del_kernel_n4_wide(int tb);
+// 16-input trellises (n0 = 4) without ones, 64 .. 1024 trellises, decode: one wave a (trellis,
+// depth-3 node) task, the trellises in LDS (trellis_wave.h): sc_del_w4.hip
+DelKern del_kernel_w4(int tb);
 
 // Kernel tables, one per translation-unit group (decode without / with guard-band ones, export),
 // so the large n0 = 3, 4 instantiations compile in parallel.  T up to 256 (one workgroup) in

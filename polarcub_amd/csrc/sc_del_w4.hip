@@ -1,0 +1,214 @@
+// sc_del_w4.hip -- deletion-channel SC decode for 16-input trellises (n0 = 4, no guard-band ones):
+// main_deletion.py's n0 = n // 3 at n = 12 .. 14 (:100), 64 .. 1024 trellises a codeword.
+//
+// Replaces BinaryPolarEncoderDecoder.decode (BinaryPolarEncoderDecoder.py:71-99, recursion
+// :223-325) over the CollectionOfBinaryTrellises of a received word
+// (VectorDistributions/CollectionOfBinaryTrellises.py:55-82, 106-129) for those shapes, with the
+// trellis levels of trellis_wave.h: one wave a (trellis, depth-3 node) task, its trellises in the
+// wave's LDS, instead of k_sc_del's one lane a trellis with 22.6 KB of private memory.
+//
+// Workgroup: 256 threads, one codeword at a time (codewords from a per-launch counter).  For each of
+// the 8 depth-3 nodes k, the four waves take the codeword's trellises in turn and leave each one's
+// three rows (minus; plus after decision 0 / 1) in LDS at its half-split position bitrev(t); wave 0
+// then decodes the memoryless node of the minus rows (16 lanes, T / 16 values a lane: the binary
+// kernel's register subtree, as k_sc_del's T >= 64 path), every trellis picks its plus row by its
+// decision, and wave 0 decodes that node.  A node whose two memoryless subtrees are both rate-0 skips
+// its tasks (its decisions are the frozen values whatever the rows).  The 16 decisions of a trellis
+// re-encode to its 16 x_hat bits (w4_enc16).
+#include <hip/hip_runtime.h>
+
+#include "sc_del_kern.h"
+#include "trellis_wave.h"
+
+namespace pcub {
+
+namespace {
+
+constexpr int kW4Waves = kDelBlock / 64;
+
+// run a phase on one lane of the wave, then make its LDS writes visible to the wave's other lanes
+struct W4WaveRun {
+    int lane;
+    template <class F>
+    __device__ __forceinline__ void operator()(F&& f) const {
+        f(lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+};
+
+template <int T>
+__device__ __forceinline__ uint64_t w4_window(const uint32_t* w, int kk, int wi) {
+    const int us = kk * T + 64 * wi;
+    return (uint64_t)w[us >> 5] | ((uint64_t)w[(us >> 5) + 1] << 32);
+}
+
+// collapse point kk's memoryless node: all frozen?
+template <int T>
+__device__ __forceinline__ bool w4_rate0(const uint32_t* fmask, int kk) {
+    bool r = true;
+    for (int i = 0; i < T / 32; ++i) r = r && fmask[kk * (T / 32) + i] == 0xffffffffu;
+    return r;
+}
+
+// SC over collapse point kk's memoryless node of the T rows vals[p] (half-split positions): wave 0,
+// 16 lanes (the other groups decode copies); bits to xb[p / 16] bit p % 16, decisions to xub
+template <int TB>
+__device__ __forceinline__ void w4_subtree(const DelArgs& A, const double* vals, int kk, unsigned long long* xb,
+                                           unsigned long long* xub) {
+    constexpr int T = 1 << TB, NW = T / 64, LV = T / 16;
+    const int lane = threadIdx.x & 63;
+    if ((threadIdx.x >> 6) == 0) {
+        uint64_t fm[NW], fv[NW], ubl[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            fm[w] = w4_window<T>(A.fmask, kk, w);
+            fv[w] = w4_window<T>(A.fval, kk, w);
+            ubl[w] = 0;
+        }
+        const int j = lane & 15;
+        double vv[LV];
+#pragma unroll
+        for (int t = 0; t < LV; ++t) vv[t] = vals[j + 16 * t];
+        typename DelWin<LV, NW>::Bits bits;
+        if constexpr (NW == 1) bits = WinTree<LV, 16, 1>::run(vv, ubl, fm, fv, lane);
+        else bits = DelWin<LV, NW>::run(vv, ubl, fm, fv, lane);
+#pragma unroll
+        for (int t = 0; t < LV; ++t) {
+            const unsigned long long bal = __ballot((bits >> t) & 1u);
+            if (lane == 0) xb[t] = bal;
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int w = 0; w < NW; ++w) xub[w] = ubl[w];
+    }
+    __syncthreads();
+}
+
+// collapse point kk's information bits (its decisions at the unfrozen positions, in order) into the
+// codeword's bit buffer at offset ib; returns the count
+template <int T>
+__device__ __forceinline__ int w4_info(const DelArgs& A, int kk, const unsigned long long* xub, uint32_t* infol, int ib) {
+    constexpr int NW = T / 64;
+    int total = 0, before = 0;
+    const int w = (int)threadIdx.x;
+    for (int i = 0; i < NW; ++i) {
+        const int c = __builtin_popcountll(~w4_window<T>(A.fmask, kk, i));
+        before += i < w ? c : 0;
+        total += c;
+    }
+    if (w < NW) {
+        const uint64_t ub = xub[w];
+        int off = ib + before;
+        for (uint64_t im = ~w4_window<T>(A.fmask, kk, w); im != 0ull; im &= im - 1ull, ++off)
+            if ((ub >> __builtin_ctzll(im)) & 1ull) atomicOr(&infol[off >> 5], 1u << (off & 31));
+    }
+    return total;
+}
+
+template <int TB>
+__global__ __launch_bounds__(kDelBlock) void k_sc_del_w4(DelArgs A) {
+    constexpr int T = 1 << TB;
+    constexpr int LV = T / 16, NW = T / 64;
+    constexpr int WPC = T / 2;  // x_hat words a codeword (16 T bits)
+    __shared__ W4Buf wb[kW4Waves];
+    __shared__ double vm[T], vp0[T], vp1[T];
+    __shared__ uint16_t hist[T], sy[T];
+    __shared__ uint8_t sm[T];
+    __shared__ uint8_t xmb[T];
+    __shared__ unsigned long long xb[LV], xub[NW];
+    __shared__ uint32_t infol[WPC];
+    __shared__ long long s_next;
+    extern __shared__ uint32_t rxb[];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (long long it = 0;; ++it) {
+        long long cw;
+        if (A.wtiles) {
+            if (threadIdx.x == 0) s_next = (long long)atomicAdd(A.wtiles, 1ull);
+            __syncthreads();
+            cw = s_next;
+        } else {
+            cw = (long long)blockIdx.x + it * (long long)gridDim.x;
+        }
+        if (cw >= A.B) break;
+        // the received word, bit-packed; each trellis's segment (m > 16: no edges)
+        pack_rows<1, kDelBlock>(A, cw, rxb, lane);
+        for (int i = threadIdx.x; i < WPC; i += kDelBlock) infol[i] = 0u;
+        __syncthreads();
+        int len = A.rx_len[cw];
+        len = len < 0 ? 0 : (len > A.stride ? A.stride : len);
+        for (int t = threadIdx.x; t < T; t += kDelBlock) {
+            int s, m;
+            segment_of_packed(rxb, len, TB, t, s, m);
+            uint32_t y = 0;
+            if (m > 0 && m <= kW4L) {
+                const int w0 = s >> 5;
+                const uint64_t lo = rxb[w0], hi = (w0 + 1 < A.rw) ? rxb[w0 + 1] : 0u;
+                y = (uint32_t)(((hi << 32) | lo) >> (s & 31)) & (uint32_t)((1u << m) - 1u);
+            }
+            sm[t] = (uint8_t)(m <= kW4L ? m : kW4L + 1);
+            sy[t] = (uint16_t)y;
+            hist[t] = 0;
+        }
+        __syncthreads();
+        int ib = 0;  // information bits so far
+#pragma unroll 1
+        for (int k = 0; k < 8; ++k) {
+            const int km = 2 * k, kp = 2 * k + 1;
+            if (!(w4_rate0<T>(A.fmask, km) && w4_rate0<T>(A.fmask, kp))) {
+#pragma unroll 1
+                for (int t = wv; t < T; t += kW4Waves) {
+                    W4Dims D;
+                    D.set(sm[t], sy[t], A.pd);
+                    w4_task(W4WaveRun{lane}, wb[wv], D, k, hist[t]);
+                    if (lane < 3) {
+                        const int p = (int)bitrev((uint32_t)t, TB);
+                        double* dst = lane == 0 ? vm : lane == 1 ? vp0 : vp1;
+                        dst[p] = wb[wv].out[lane];
+                    }
+                }
+            }
+            __syncthreads();
+            // the minus node, then every position's plus row by its decision, then the plus node
+            w4_subtree<TB>(A, vm, km, xb, xub);
+            ib += w4_info<T>(A, km, xub, infol, ib);
+            for (int p = threadIdx.x; p < T; p += kDelBlock) {
+                const uint32_t x = (uint32_t)(xb[p >> 4] >> (p & 15)) & 1u;
+                xmb[p] = (uint8_t)x;
+                vm[p] = x ? vp1[p] : vp0[p];
+            }
+            __syncthreads();
+            w4_subtree<TB>(A, vm, kp, xb, xub);
+            ib += w4_info<T>(A, kp, xub, infol, ib);
+            for (int t = threadIdx.x; t < T; t += kDelBlock) {
+                const int p = (int)bitrev((uint32_t)t, TB);
+                const uint32_t xp = (uint32_t)(xb[p >> 4] >> (p & 15)) & 1u;
+                hist[t] = (uint16_t)(hist[t] | ((uint32_t)xmb[p] << km) | (xp << kp));
+            }
+            __syncthreads();
+        }
+        // x_hat: trellis t's slice is natural positions [16 t, 16 t + 16)
+        if (A.xhat)
+            for (int i = threadIdx.x; i < WPC; i += kDelBlock)
+                A.xhat[(long long)i * A.B + cw] = w4_enc16(hist[2 * i]) | (w4_enc16(hist[2 * i + 1]) << 16);
+        if (A.info)
+            for (int i = threadIdx.x; i < (ib + 31) / 32; i += kDelBlock) A.info[(long long)i * A.B + cw] = infol[i];
+        __syncthreads();  // rxb / sm / hist / infol are rewritten by the next codeword
+    }
+}
+
+}  // namespace
+
+DelKern del_kernel_w4(int tb) {
+    switch (tb) {
+        case 6: return k_sc_del_w4<6>;
+        case 7: return k_sc_del_w4<7>;
+        case 8: return k_sc_del_w4<8>;
+        case 9: return k_sc_del_w4<9>;
+        case 10: return k_sc_del_w4<10>;
+        default: return nullptr;
+    }
+}
+
+}  // namespace pcub

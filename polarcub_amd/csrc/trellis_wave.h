@@ -1,0 +1,524 @@
+// trellis_wave.h -- the n0 = 4 deletion trellises computed by a whole wave (host + device).
+//
+// Restates, for 16-input trellises without guard-band ones (main_deletion.py's n0 = n // 3 at
+// n = 12 .. 14, :100):
+//   BinaryTrellis.__miusPlusTransform                 VectorDistributions/BinaryTrellis.py:206-258
+//   BinaryTrellis.calcNormalizationVector / normalize VectorDistributions/BinaryTrellis.py:280-306
+//   the collection collapse                           VectorDistributions/CollectionOfBinaryTrellises.py:68-82
+// with the same values and the same order of every floating-point sum as trellis_body.h's Trel walk
+// (DelBase / DelNode, sc_del_kern.h), which tests/emu/w4_check.cpp compares bit for bit.
+//
+// Task.  A trellis's SC walk visits 8 depth-3 nodes; node k's length-2 trellis is a function of the
+// segment (m <= 16 received bits) and of the decisions returned before it (the re-encodings that
+// select the plus transforms on its path).  One task = (trellis, k): build the depth-1, depth-2 and
+// depth-3 trellises on node k's path from the implicit base (BaseT), then its three collapsed rows:
+// the minus row, and the plus row for either decision of the minus subtree.  Nothing persists between
+// tasks but the 16 decision bits, so a codeword's 2^(n-4) trellises need no per-trellis storage
+// (the lane-serial Trel kernel kept 22.6 KB of private memory a trellis).
+//
+// Layout.  One wave a task, its trellises in the wave's LDS region (W4Buf), lanes over edge slots.
+// A depth-d trellis's edge (layer j, from u, advance a, label x) sits at a fixed slot: u's offset in
+// the layer's window [lo, hi] (lo = max(0, j 2^d - dd), hi = min(j 2^d, m), dd = 16 - m deletions),
+// a - amin(d) with a in [amin(d), amin(d) + na(d)) (amin = max(0, 2^d - dd), na = min(2^d, dd) + 1),
+// and x: pw * na(d) * 2 slots a layer, pw = min(dd, m) + 1 window positions (trellis_dense.h's
+// capacity argument).  A child edge's sum is a gather: its contributions come from middle vertices w
+// (u -> w -> v), and the reference adds them in its iteration order -- middle vertices in insertion
+// order, then in-edges of w in creation order, then out-edges in creation order -- so a slot walks
+// the middle layer's vertices by insertion rank and, per w, its (at most two) in-edges by creation
+// rank.  The orders themselves are ranks:
+//   * an edge is created by its first contribution, so its creation rank is the rank of the key
+//     (rank of w, creation rank of the in-edge, creation rank of the out-edge) of that contribution
+//     among the layer's edges;
+//   * a vertex of a middle layer l is inserted by its first reference: as the to-vertex of an edge of
+//     layer l - 1 (all of layer l - 1's adds come first), else as the from-vertex of one of layer l;
+//     its insertion rank is the rank of (phase, least creation rank);
+//   * the normaliser of a layer sums, per label, the edges in (from-vertex rank, creation rank) order.
+// Sums whose order matters are taken by one lane in that order; zero terms padded after a sum's last
+// term (x + 0.0 == x for the non-negative sums here) keep their trip counts regular.
+#pragma once
+#include "trellis_body.h"
+
+namespace pcub {
+
+constexpr int kW4L = 16;      // base trellis length
+constexpr int kW4PW = 9;      // window positions a layer, at most (min(dd, m) + 1)
+constexpr int kW4SA = 432;    // region A: depth 1 (8 x 9 x 3 x 2) or depth 3 (2 x 9 x 9 x 2)
+constexpr int kW4SB = 360;    // region B: depth 2 (4 x 9 x 5 x 2)
+constexpr uint32_t kW4None = 0xffffffffu;
+constexpr uint8_t kW4NoC = 0xffu;
+constexpr uint16_t kW4NoV = 0xffffu;
+
+// a segment: m received symbols (m <= 16), bits y, the channel's edge probabilities
+struct W4Dims {
+    int m, dd, pw;
+    uint32_t y;
+    double pins, pdel;
+    PCUB_HD void set(int m_, uint32_t y_, double pd) {
+        m = m_;
+        dd = kW4L - m_;
+        pw = (dd < m_ ? dd : m_) + 1;
+        y = y_;
+        pins = 0.5 * (1.0 - pd);
+        pdel = 0.5 * pd;
+    }
+    PCUB_HD int lo(int b) const { return b - dd > 0 ? b - dd : 0; }
+    PCUB_HD int hi(int b) const { return b < m ? b : m; }
+    PCUB_HD int na(int d) const { return ((1 << d) < dd ? (1 << d) : dd) + 1; }
+    PCUB_HD int amin(int d) const { return (1 << d) - dd > 0 ? (1 << d) - dd : 0; }
+    PCUB_HD int sl(int d) const { return pw * na(d) * 2; }
+    // the base trellis (buildTrellis_uniformInput_deletion, BinaryTrellis.py:384-436; BaseT)
+    PCUB_HD bool b_in(int l, int vp) const { return vp >= lo(l) && vp <= hi(l); }
+    PCUB_HD bool b_ins(int l, int vp) const { return b_in(l, vp) && vp < m; }
+    PCUB_HD bool b_del(int l, int vp) const { return b_in(l, vp) && vp >= lo(l + 1); }
+    PCUB_HD int ybit(int vp) const { return (int)((y >> vp) & 1u); }
+    PCUB_HD double p_del(int vp, int lbl) const { return (lbl == 0 && !(vp > 0 && vp < m)) ? 0.5 : pdel; }
+    // creation rank of base edge (l, vp, kind): kind 0 insertion, 1 deletion of a 0, 2 of a 1; the
+    // layer creates, for vp ascending, the insertion and then the two deletions
+    PCUB_HD int b_crank(int l, int vp, int kind) const {
+        const int a = lo(l), a1 = lo(l + 1);
+        const int mi = vp < m ? vp : m;
+        const int nins = mi - a > 0 ? mi - a : 0;
+        const int ds = a > a1 ? a : a1;
+        const int ndel = vp - ds > 0 ? 2 * (vp - ds) : 0;
+        return nins + ndel + (kind == 0 ? 0 : (vp < m ? 1 : 0) + (kind - 1));
+    }
+    // insertion rank of vertex w of base layer l (1 <= l < 16) among those with in-edges (BaseT::reached)
+    PCUB_HD int b_vrank(int l, int w) const {
+        const int a = lo(l - 1);
+        const int c0 = a < m ? 1 : 0;
+        const int c1 = l - dd <= a ? 1 : 0;
+        const int last = hi(l - 1) < m - 1 ? hi(l - 1) : m - 1;
+        if (c0 && w == a + 1) return 0;
+        if (c1 && w == a) return c0;
+        if (w >= a + 2 && w <= last + 1) return c0 + c1 + (w - a - 2);
+        return -1;
+    }
+};
+
+// one wave's trellises (LDS on the device)
+struct W4Buf {
+    double pA[kW4SA];        // region A: depth 1, later depth 3 (probabilities)
+    uint32_t kA[kW4SA];      // ... first-contribution keys
+    double pB[kW4SB];        // region B: depth 2
+    uint32_t kB[kW4SB];
+    uint8_t cA[kW4SA];       // creation ranks (kW4NoC: no edge)
+    uint8_t cB[kW4SB];
+    uint8_t vrA[9][kW4PW];   // vertex insertion rank per window offset (kW4NoC: absent), layers 0..8
+    uint8_t voA[9][kW4PW];   // window offset of the vertex of each rank
+    uint8_t nvA[9];
+    uint8_t vrB[5][kW4PW];
+    uint8_t voB[5][kW4PW];
+    uint8_t nvB[5];
+    uint16_t vkey[8][kW4PW];  // vertex keys of the layer being ranked
+    uint32_t ncnt[8][2];      // edges a (layer, label) of the layer being normalised
+    double sums[8][2];        // normalisation sums
+    double out[3];            // the task's rows: minus, plus after 0, plus after 1
+};
+
+// a depth-d trellis in one of the regions
+struct W4View {
+    double* p;
+    uint32_t* k;
+    uint8_t* c;
+    uint8_t (*vr)[kW4PW];
+    uint8_t (*vo)[kW4PW];
+    uint8_t* nv;
+    double* tmp;  // normalisation scratch: the other region (>= this trellis's slot count doubles)
+};
+
+PCUB_HD W4View w4_view_a(W4Buf& b) { return W4View{b.pA, b.kA, b.cA, b.vrA, b.voA, b.nvA, b.pB}; }
+PCUB_HD W4View w4_view_b(W4Buf& b) { return W4View{b.pB, b.kB, b.cB, b.vrB, b.voB, b.nvB, b.pA}; }
+
+// ---- phase 1 of a transform: child edges (values and first-contribution keys) ----
+
+// depth-1 child (layer j, window offset uo, advance offset ao) from the implicit base: the middle
+// vertices are w = u (in-edges: the deletions) and w = u + 1 (the insertion), by base insertion rank
+PCUB_HD void w4_base_item(const W4Dims& D, const W4View& C, int j, int uo, int ao, int dj, bool plus) {
+    const int NA = D.na(1), SL = D.sl(1);
+    const int s = j * SL + (uo * NA + ao) * 2;
+    double acc[2] = {0.0, 0.0};
+    uint32_t key[2] = {kW4None, kW4None};
+    const int l0 = 2 * j, l1 = 2 * j + 1;
+    const int u = D.lo(l0) + uo;
+    if (u <= D.hi(l0)) {
+        const int v = u + D.amin(1) + ao;
+        int wv[2], rk[2], nw = 0;
+        for (int a1 = 0; a1 < 2; ++a1) {
+            const int w = u + a1, a2 = v - w;
+            if (a2 < 0 || a2 > 1) continue;
+            const int r = D.b_vrank(l1, w);
+            if (r < 0) continue;
+            wv[nw] = w;
+            rk[nw] = r;
+            ++nw;
+        }
+        if (nw == 2 && rk[1] < rk[0]) {
+            const int t = wv[0]; wv[0] = wv[1]; wv[1] = t;
+            const int q = rk[0]; rk[0] = rk[1]; rk[1] = q;
+        }
+        for (int i = 0; i < nw; ++i) {
+            const int w = wv[i], a1 = w - u, a2 = v - w;
+            // in-edges u -> w in creation order
+            int na = 0, la[2], ca[2];
+            double pa[2];
+            if (a1 == 0) {
+                if (D.b_del(l0, u)) {
+                    for (int x = 0; x < 2; ++x) {
+                        la[na] = x;
+                        pa[na] = D.p_del(u, x);
+                        ca[na] = D.b_crank(l0, u, 1 + x);
+                        ++na;
+                    }
+                }
+            } else if (D.b_ins(l0, u)) {
+                la[0] = D.ybit(u);
+                pa[0] = D.pins;
+                ca[0] = D.b_crank(l0, u, 0);
+                na = 1;
+            }
+            // out-edges w -> v, by label
+            bool eb[2] = {false, false};
+            double pb[2] = {0.0, 0.0};
+            int cb[2] = {0, 0};
+            if (a2 == 0) {
+                if (D.b_del(l1, w))
+                    for (int x = 0; x < 2; ++x) {
+                        eb[x] = true;
+                        pb[x] = D.p_del(w, x);
+                        cb[x] = D.b_crank(l1, w, 1 + x);
+                    }
+            } else if (D.b_ins(l1, w)) {
+                const int yb = D.ybit(w);
+                eb[yb] = true;
+                pb[yb] = D.pins;
+                cb[yb] = D.b_crank(l1, w, 0);
+            }
+            for (int ia = 0; ia < na; ++ia)
+                for (int x = 0; x < 2; ++x) {
+                    int lb;
+                    if (plus) {
+                        lb = x;
+                        if ((la[ia] ^ lb) != dj) continue;
+                    } else {
+                        lb = la[ia] ^ x;
+                    }
+                    if (!eb[lb]) continue;
+                    acc[x] += pa[ia] * pb[lb];
+                    if (key[x] == kW4None) key[x] = ((uint32_t)rk[i] << 16) | ((uint32_t)ca[ia] << 8) | (uint32_t)cb[lb];
+                }
+        }
+    }
+    for (int x = 0; x < 2; ++x) {
+        C.p[s + x] = acc[x];
+        C.k[s + x] = key[x];
+    }
+}
+
+// depth-(d+1) child (layer j, uo, ao) of the depth-d parent P: walk P's middle layer 2j + 1 by
+// insertion rank; per w, the in-edges (u, w - u) by creation rank, each with its out-edge to v
+PCUB_HD void w4_item(const W4Dims& D, int d, const W4View& P, const W4View& C, int j, int uo, int ao, int dj,
+                     bool plus) {
+    const int NAc = D.na(d + 1), SLc = D.sl(d + 1);
+    const int NAp = D.na(d), SLp = D.sl(d), AMp = D.amin(d);
+    const int s = j * SLc + (uo * NAc + ao) * 2;
+    double acc[2] = {0.0, 0.0};
+    uint32_t key[2] = {kW4None, kW4None};
+    const int u = D.lo((2 * j) << d) + uo;
+    if (u <= D.hi((2 * j) << d)) {
+        const int v = u + D.amin(d + 1) + ao;
+        const int mv = 2 * j + 1;
+        const int wlo = D.lo(mv << d);
+        const int nvm = P.nv[mv];
+        for (int r = 0; r < nvm; ++r) {
+            const int wo = P.vo[mv][r];
+            const int w = wlo + wo;
+            const int a1 = w - u - AMp, a2 = v - w - AMp;
+            if (a1 < 0 || a1 >= NAp || a2 < 0 || a2 >= NAp) continue;
+            const int ia = (2 * j) * SLp + (uo * NAp + a1) * 2;
+            const int ib = (2 * j + 1) * SLp + (wo * NAp + a2) * 2;
+            const int ca0 = P.c[ia], ca1 = P.c[ia + 1];
+            const int cb0 = P.c[ib], cb1 = P.c[ib + 1];
+            const int f = (ca1 < ca0) ? 1 : 0;  // the in-edge created first (kW4NoC sorts last)
+            for (int t = 0; t < 2; ++t) {
+                const int la = f ^ t;
+                const int ca = la ? ca1 : ca0;
+                if (ca == kW4NoC) continue;
+                const double pa = P.p[ia + la];
+                for (int x = 0; x < 2; ++x) {
+                    int lb;
+                    if (plus) {
+                        lb = x;
+                        if ((la ^ lb) != dj) continue;
+                    } else {
+                        lb = la ^ x;
+                    }
+                    const int cb = lb ? cb1 : cb0;
+                    if (cb == kW4NoC) continue;
+                    acc[x] += pa * P.p[ib + lb];
+                    if (key[x] == kW4None) key[x] = ((uint32_t)r << 16) | ((uint32_t)ca << 8) | (uint32_t)cb;
+                }
+            }
+        }
+    }
+    for (int x = 0; x < 2; ++x) {
+        C.p[s + x] = acc[x];
+        C.k[s + x] = key[x];
+    }
+}
+
+// ---- the phases (lane-strided loops; a wave barrier between consecutive phases) ----
+
+// child edges of the transform into depth d + 1 (d = 0: from the base)
+PCUB_HD void w4_ph_edges(const W4Dims& D, int d, const W4View& P, const W4View& C, uint32_t dec, bool plus,
+                         int lane) {
+    const int LEN = kW4L >> (d + 1);
+    const int NA = D.na(d + 1);
+    const int per = D.pw * NA;
+    for (int i = lane; i < LEN * per; i += 64) {
+        const int j = i / per, r = i - j * per;
+        const int uo = r / NA, ao = r - uo * NA;
+        const int dj = (int)((dec >> j) & 1u);
+        if (d == 0) w4_base_item(D, C, j, uo, ao, dj, plus);
+        else w4_item(D, d, P, C, j, uo, ao, dj, plus);
+    }
+}
+
+// creation ranks of the child's edges; zero the normalisation counters
+PCUB_HD void w4_ph_rank(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
+    const int LEN = kW4L >> dc, SL = D.sl(dc);
+    for (int s = lane; s < LEN * SL; s += 64) {
+        const uint32_t k = C.k[s];
+        uint8_t c = kW4NoC;
+        if (k != kW4None) {
+            const int j = s / SL;
+            int n = 0;
+            for (int t = j * SL; t < (j + 1) * SL; ++t) n += C.k[t] < k ? 1 : 0;
+            c = (uint8_t)n;
+        }
+        C.c[s] = c;
+    }
+    if (lane < 16) b.ncnt[lane >> 1][lane & 1] = 0u;
+}
+
+// vertex keys of the child's layers 1 .. LEN-1 (D3: layer 1 only); zero the normalisation scratch
+PCUB_HD void w4_ph_vkey(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
+    const int LEN = kW4L >> dc, SL = D.sl(dc), NA = D.na(dc), AM = D.amin(dc);
+    const int nl = LEN - 1;
+    for (int i = lane; i < nl * D.pw; i += 64) {
+        const int l = 1 + i / D.pw, po = i % D.pw;
+        const int p = D.lo(l << dc) + po;
+        uint16_t vk = kW4NoV;
+        if (p <= D.hi(l << dc)) {
+            int k0 = 0xffff;
+            const int plo = D.lo((l - 1) << dc);
+            for (int ao = 0; ao < NA; ++ao) {
+                const int uo = p - AM - ao - plo;
+                if (uo < 0 || uo >= D.pw) continue;
+                const int s = (l - 1) * SL + (uo * NA + ao) * 2;
+                for (int x = 0; x < 2; ++x) {
+                    const int c = C.c[s + x];
+                    if (c != kW4NoC && c < k0) k0 = c;
+                }
+            }
+            if (k0 != 0xffff) {
+                vk = (uint16_t)k0;
+            } else {
+                int k1 = 0xffff;
+                for (int t = 0; t < NA * 2; ++t) {
+                    const int c = C.c[l * SL + po * NA * 2 + t];
+                    if (c != kW4NoC && c < k1) k1 = c;
+                }
+                if (k1 != 0xffff) vk = (uint16_t)(256 + k1);
+            }
+        }
+        b.vkey[l - 1][po] = vk;
+    }
+    const int total = LEN * SL;
+    for (int i = lane; i < total; i += 64) C.tmp[i] = 0.0;
+}
+
+// vertex insertion ranks from the keys (layer 0: the start vertex alone)
+PCUB_HD void w4_ph_vrank(const W4Dims& D, int dc, const W4View& C, const W4Buf& b, int lane) {
+    const int LEN = kW4L >> dc;
+    const int nl = LEN - 1;
+    for (int i = lane; i < nl * D.pw; i += 64) {
+        const int l = 1 + i / D.pw, po = i % D.pw;
+        const uint16_t vk = b.vkey[l - 1][po];
+        int r = 0, nv = 0;
+        for (int t = 0; t < D.pw; ++t) {
+            const uint16_t o = b.vkey[l - 1][t];
+            r += o < vk ? 1 : 0;
+            nv += o != kW4NoV ? 1 : 0;
+        }
+        if (vk != kW4NoV) {
+            C.vr[l][po] = (uint8_t)r;
+            C.vo[l][r] = (uint8_t)po;
+        } else {
+            C.vr[l][po] = kW4NoC;
+        }
+        if (po == 0) C.nv[l] = (uint8_t)nv;
+    }
+    if (lane == 0) {
+        C.vr[0][0] = 0;
+        C.vo[0][0] = 0;
+        C.nv[0] = 1;
+    }
+}
+
+// normalisation order: each edge's position among its layer's same-label edges by
+// (from-vertex rank, creation rank), its probability scattered there
+PCUB_HD void w4_ph_norder(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
+    const int LEN = kW4L >> dc, SL = D.sl(dc), NA = D.na(dc);
+    const int half = SL / 2;
+    for (int s = lane; s < LEN * SL; s += 64) {
+        const int c = C.c[s];
+        if (c == kW4NoC) continue;
+        const int j = s / SL, r = s - j * SL, x = r & 1;
+        const int key = (C.vr[j][(r >> 1) / NA] << 8) | c;
+        int n = 0;
+        for (int t = x; t < SL; t += 2) {
+            const int c2 = C.c[j * SL + t];
+            if (c2 == kW4NoC) continue;
+            const int k2 = (C.vr[j][(t >> 1) / NA] << 8) | c2;
+            n += k2 < key ? 1 : 0;
+        }
+        C.tmp[j * SL + x * half + n] = C.p[s];
+#if defined(__HIP_DEVICE_COMPILE__)
+        atomicAdd(&b.ncnt[j][x], 1u);
+#else
+        ++b.ncnt[j][x];
+#endif
+    }
+}
+
+// the per-(layer, label) sums, each by one lane in order (4 terms a step: the zeros after the last
+// term change nothing)
+PCUB_HD void w4_ph_nsum(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
+    const int LEN = kW4L >> dc, SL = D.sl(dc);
+    if (lane < 2 * LEN) {
+        const int j = lane >> 1, x = lane & 1;
+        const double* t = C.tmp + j * SL + x * (SL / 2);
+        const int n = (int)b.ncnt[j][x];
+        double s = 0.0;
+        for (int i = 0; i < n; i += 4) {
+            const double t0 = t[i], t1 = i + 1 < SL / 2 ? t[i + 1] : 0.0, t2 = i + 2 < SL / 2 ? t[i + 2] : 0.0,
+                         t3 = i + 3 < SL / 2 ? t[i + 3] : 0.0;
+            s += t0;
+            s += t1;
+            s += t2;
+            s += t3;
+        }
+        b.sums[j][x] = s;
+    }
+}
+
+// normalize: every edge of layer j divided by max(s0, s1) (1 when both are 0)
+PCUB_HD void w4_ph_ndiv(const W4Dims& D, int dc, const W4View& C, const W4Buf& b, int lane) {
+    const int LEN = kW4L >> dc, SL = D.sl(dc);
+    for (int s = lane; s < LEN * SL; s += 64) {
+        if (C.c[s] == kW4NoC) continue;
+        const int j = s / SL;
+        const double s0 = b.sums[j][0], s1 = b.sums[j][1];
+        double dv = s0 >= s1 ? s0 : s1;
+        if (dv == 0.0) dv = 1.0;
+        C.p[s] = C.p[s] / dv;
+    }
+}
+
+// the three collapsed rows of the depth-3 trellis (lanes 0, 1, 2: minus, plus after 0, plus after 1)
+PCUB_HD void w4_ph_collapse(const W4Dims& D, const W4View& C, W4Buf& b, int lane) {
+    if (lane >= 3) return;
+    const int NA = D.na(3), SL = D.sl(3), AM = D.amin(3);
+    const int wlo = D.lo(8);
+    double m0 = 0.0, m1 = 0.0;
+    const int nv1 = C.nv[1];
+    for (int r = 0; r < nv1; ++r) {
+        const int wo = C.vo[1][r];
+        const int w = wlo + wo;
+        const int a1 = w - AM, a2 = D.m - w - AM;
+        if (a1 < 0 || a1 >= NA || a2 < 0 || a2 >= NA) continue;
+        const int ia = a1 * 2;                       // layer 0, from vertex 0 (offset 0)
+        const int ib = SL + (wo * NA + a2) * 2;      // layer 1, to vertex m
+        const int ca0 = C.c[ia], ca1 = C.c[ia + 1], cb0 = C.c[ib], cb1 = C.c[ib + 1];
+        const int fa = ca1 < ca0 ? 1 : 0, fb = cb1 < cb0 ? 1 : 0;
+        for (int t = 0; t < 2; ++t) {
+            const int la = fa ^ t;
+            if ((la ? ca1 : ca0) == kW4NoC) continue;
+            const double pa = C.p[ia + la];
+            for (int q = 0; q < 2; ++q) {
+                const int lb = fb ^ q;
+                if ((lb ? cb1 : cb0) == kW4NoC) continue;
+                const double prob = pa * C.p[ib + lb];
+                const int ml = la ^ lb;
+                int x = ml;
+                if (lane > 0) {
+                    if (ml != lane - 1) continue;
+                    x = lb;
+                }
+                if (x) m1 += prob;
+                else m0 += prob;
+            }
+        }
+    }
+    b.out[lane] = norm_pack(m0, m1);
+}
+
+// The re-encoding of a node's returned bits: x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h] (DelNode)
+PCUB_HD uint32_t w4_combine(uint32_t ym, uint32_t yp, int H) {
+    uint32_t x = 0;
+    for (int h = 0; h < H; ++h) x |= ((((ym ^ yp) >> h) & 1u) << (2 * h)) | (((yp >> h) & 1u) << (2 * h + 1));
+    return x;
+}
+// node i's two bits (depth 3) -> its 2-bit encoding
+PCUB_HD uint32_t w4_enc2(uint32_t hist, int i) {
+    const uint32_t xm = (hist >> (2 * i)) & 1u, xp = (hist >> (2 * i + 1)) & 1u;
+    return (xm ^ xp) | (xp << 1);
+}
+PCUB_HD uint32_t w4_enc4(uint32_t hist, int i) { return w4_combine(w4_enc2(hist, 2 * i), w4_enc2(hist, 2 * i + 1), 2); }
+PCUB_HD uint32_t w4_enc8(uint32_t hist, int i) { return w4_combine(w4_enc4(hist, 2 * i), w4_enc4(hist, 2 * i + 1), 4); }
+PCUB_HD uint32_t w4_enc16(uint32_t hist) { return w4_combine(w4_enc8(hist, 0), w4_enc8(hist, 1), 8); }
+
+// One task: depth-3 node k of a segment with decision history hist (bit 2i / 2i+1: the minus / plus
+// subtree of node i < k).  `run(f)` runs f(lane) on every lane of the wave, then a wave barrier.
+// Leaves b.out[0..2] = the minus row, the plus row after decision 0, after decision 1.
+template <class Run>
+PCUB_HD void w4_task(const Run& run, W4Buf& b, const W4Dims& D, int k, uint32_t hist) {
+    if (D.m > kW4L) {  // no edges (BaseT with m > L): every row is the collapse of an empty trellis
+        run([&](int lane) {
+            if (lane < 3) b.out[lane] = norm_pack(0.0, 0.0);
+        });
+        return;
+    }
+    const W4View A = w4_view_a(b), B = w4_view_b(b);
+    const bool p1 = (k >> 2) & 1, p2 = (k >> 1) & 1, p3 = k & 1;
+    const uint32_t d1 = p1 ? w4_enc8(hist, 0) : 0u;
+    const uint32_t d2 = p2 ? w4_enc4(hist, (k >> 1) - 1) : 0u;
+    const uint32_t d3 = p3 ? w4_enc2(hist, k - 1) : 0u;
+    // depth 1 (region A) from the base
+    run([&](int lane) { w4_ph_edges(D, 0, A, A, d1, p1, lane); });
+    run([&](int lane) { w4_ph_rank(D, 1, A, b, lane); });
+    run([&](int lane) { w4_ph_vkey(D, 1, A, b, lane); });
+    run([&](int lane) { w4_ph_vrank(D, 1, A, b, lane); });
+    run([&](int lane) { w4_ph_norder(D, 1, A, b, lane); });
+    run([&](int lane) { w4_ph_nsum(D, 1, A, b, lane); });
+    run([&](int lane) { w4_ph_ndiv(D, 1, A, b, lane); });
+    // depth 2 (region B)
+    run([&](int lane) { w4_ph_edges(D, 1, A, B, d2, p2, lane); });
+    run([&](int lane) { w4_ph_rank(D, 2, B, b, lane); });
+    run([&](int lane) { w4_ph_vkey(D, 2, B, b, lane); });
+    run([&](int lane) { w4_ph_vrank(D, 2, B, b, lane); });
+    run([&](int lane) { w4_ph_norder(D, 2, B, b, lane); });
+    run([&](int lane) { w4_ph_nsum(D, 2, B, b, lane); });
+    run([&](int lane) { w4_ph_ndiv(D, 2, B, b, lane); });
+    // depth 3 (region A again)
+    run([&](int lane) { w4_ph_edges(D, 2, B, A, d3, p3, lane); });
+    run([&](int lane) { w4_ph_rank(D, 3, A, b, lane); });
+    run([&](int lane) { w4_ph_vkey(D, 3, A, b, lane); });
+    run([&](int lane) { w4_ph_vrank(D, 3, A, b, lane); });
+    run([&](int lane) { w4_ph_norder(D, 3, A, b, lane); });
+    run([&](int lane) { w4_ph_nsum(D, 3, A, b, lane); });
+    run([&](int lane) { w4_ph_ndiv(D, 3, A, b, lane); });
+    run([&](int lane) { w4_ph_collapse(D, A, b, lane); });
+}
+
+}  // namespace pcub

@@ -696,6 +696,17 @@ def set_deletion_rate1(on):
     return int(f(int(on)))
 
 
+def set_deletion_wave(on):
+    """Diagnostic: 0 sends n0 = 4 deletion decodes (64 .. 1024 trellises) back to the lane-per-trellis
+    kernel instead of the wave-per-task kernel (pcub_sc_set_deletion_wave, not part of the stable ABI);
+    returns the previous setting.  Decisions are identical either way."""
+    import ctypes
+    f = _lib.lib().pcub_sc_set_deletion_wave
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int32]
+    return int(f(int(on)))
+
+
 def set_dynamic_tiles(on):
     """Diagnostic: 0 makes the binary, q-ary and deletion decode kernels stride over their tiles
     statically instead of taking them from a per-launch counter (pcub_sc_set_dynamic_tiles, not part of

@@ -190,3 +190,17 @@ def test_dense_trellis_matches_trel():
         r = subprocess.run([exe, "100000", str(seed)], capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stdout + r.stderr
         assert " 0 mismatches" in r.stdout
+
+
+def test_wave_trellises_match_trel():
+    """trellis_wave.h (the n0 = 4 wave-per-task trellises of sc_del_w4.hip: edges at fixed slots, the
+    reference's creation and insertion orders as ranks of first contributions) against
+    trellis_body.h's Trel walk on random segments (lengths 0..16 and beyond, pd from 0 to 1) and random
+    decision histories: every depth-3 node's three collapsed rows bit-identical, and the re-encoding of
+    the 16 decisions equal to the recursion's (tests/emu/w4_check.cpp, its lanes run one after another)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "emu")], check=True)
+    exe = os.path.join(ROOT, "tests", "emu", "build", "w4_check")
+    for seed in (21, 22):
+        r = subprocess.run([exe, "20000", str(seed)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert " 0 mismatches" in r.stdout

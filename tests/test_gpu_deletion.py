@@ -118,6 +118,53 @@ def test_wide_shapes_vs_c_oracle(sc, n):
     assert np.array_equal(xhat, x_ref)
 
 
+@pytest.mark.parametrize("n", [10, 11, 12, 13, 14])
+def test_wave_kernel_matches_lane_kernel(sc, n):
+    """n0 = 4 (main_deletion's n0 = n // 3 at n = 12 .. 14): the wave-per-task kernel
+    (sc_del_w4.hip, trellis_wave.h) against the lane-per-trellis kernel k_sc_del and the C oracle
+    (oracle/trellis_oracle.c): channel outputs at pd 0.05 .. 0.4 (segments from 0 to 16 symbols and
+    overlong ones), an empty, a one-symbol, an all-zeros and an overlong random word, a frozen set
+    with rate-0 depth-3 nodes (their tasks skipped) and one with none.  Bit-exact."""
+    from oracle import orc
+    n0 = 4
+    N = 1 << n
+    rng = np.random.default_rng(500 + n)
+    prng = random.Random(900 + n)
+    for fs in range(2):
+        if fs == 0:
+            frozen = (rng.random(N) < 0.5).astype(np.uint8)
+            frozen[: N // 4] = 1  # the first four collapse points' nodes are rate-0
+        else:
+            frozen = (rng.random(N) < 0.3).astype(np.uint8)
+            frozen[:: N // 16] = 0  # no rate-0 node
+        fval = (rng.random(N) < 0.5).astype(np.uint8)
+        pd = (0.05, 0.1, 0.25, 0.4)[(n + fs) % 4]
+        words = []
+        for t in range(6):
+            x = [int(b) for b in rng.integers(0, 2, N)]
+            cw = tro.add_guard_bands(x, n, n0, 0.1, 0)
+            words.append(tro.deletion_channel(cw, (0.05, 0.1, 0.2, 0.3, 0.4, 0.1)[t], prng))
+        words += [[], [1], [0] * 9, [int(b) for b in rng.integers(0, 2, N + N // 2)]]
+        W = max(len(w) for w in words)
+        rx = np.zeros((len(words), W), np.uint8)
+        for i, w in enumerate(words):
+            rx[i, :len(w)] = w
+        ln = np.array([len(w) for w in words], np.int32)
+        old = sc.set_deletion_wave(1)
+        try:
+            info_w, xhat_w = _dec(sc, n, n0, pd, frozen, fval, rx, ln)
+            sc.set_deletion_wave(0)
+            info_l, xhat_l = _dec(sc, n, n0, pd, frozen, fval, rx, ln)
+        finally:
+            sc.set_deletion_wave(old)
+        assert np.array_equal(info_w, info_l), (n, fs)
+        assert np.array_equal(xhat_w, xhat_l), (n, fs)
+        if n <= 12:
+            i_ref, x_ref = orc.decode_deletion(rx, ln, n, n0, pd, frozen, fval)
+            assert np.array_equal(info_w, i_ref), (n, fs)
+            assert np.array_equal(xhat_w, x_ref), (n, fs)
+
+
 def test_ragged_batches_match_single(sc):
     """A large batch (padding groups in the last workgroup) equals per-codeword results."""
     g = load_golden("deletion_n8")

@@ -17,6 +17,7 @@
 #include "polarcub_sc.h"
 #include "sc_del_dense.h"
 #include "sc_del_kern.h"
+#include "trellis_wave.h"
 
 using namespace pcub;
 
@@ -216,18 +217,30 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     const long long rw = ((long long)stride + 31) / 32;
     // n0 = 4 without ones (main_deletion's n = 12 .. 14): one wave a (trellis, depth-3 node) task, the
     // trellises in LDS (sc_del_w4.hip), codewords from a per-launch counter
-    if (!exp && n0 == 4 && ones == 0 && g_wave4.load(std::memory_order_relaxed) && rw * 4 <= kW4MaxRxLds) {
-        const DelKern wk = del_kernel_w4(n - n0);
+    // (at 512 / 1024 trellises, n = 13 / 14, the lane kernel is still faster: 16.8 / 9.9 k against 11.7 / 5.8 k
+    // cw/s; the wave kernel takes them when asked, pcub_sc_set_deletion_wave(2))
+    const int w4m = g_wave4.load(std::memory_order_relaxed);
+    if (!exp && n0 == 4 && ones == 0 && w4m && (n - n0 <= 8 || w4m == 2) && rw * 4 <= kW4MaxRxLds) {
+        const DelKern wk = del_kernel_w4(n - n0, 0);
         if (wk) {
             A.rw = (int)rw;
+            A.gate_id = w4m == 3 ? 1ull : 0ull;  // diagnostics: tasks skipped
             const size_t lds = (size_t)(rw * 4);
             const long long grid = resident_grid(wk, lds, B);
             if (pcub_sc_dynamic_tiles()) {
                 const int rc = counter_slot(&A.wtiles, (hipStream_t)stream);
                 if (rc) return rc;
             }
+            // the per-trellis depth-1 / depth-2 caches of the resident workgroups (trellis_wave.h), a
+            // stream-ordered workspace in the export-only leaf slot (this kernel never exports)
+            void* ws = nullptr;
+            hipError_t e = hipMallocAsync(&ws, (size_t)grid * ((size_t)1 << (n - n0)) * kW4Cache, (hipStream_t)stream);
+            if (e != hipSuccess) return (int)e;
+            A.leaf = (double*)ws;
             hipLaunchKernelGGL(wk, dim3((unsigned)grid), dim3(kDelBlock), lds, (hipStream_t)stream, A);
-            return (int)hipGetLastError();
+            const int rc = (int)hipGetLastError();
+            e = hipFreeAsync(ws, (hipStream_t)stream);
+            return rc ? rc : (int)e;
         }
     }
     const bool dense = !exp && use_dense(n, n0, ones, stride, table);
@@ -341,10 +354,11 @@ extern "C" int pcub_sc_set_deletion_lanes(int32_t g) {
 // of DESIGN 3.2.  Decisions are identical either way.  Returns the previous setting.
 extern "C" int pcub_sc_set_deletion_rate1(int32_t on) { return g_dense_rate1.exchange(on ? 1 : 0); }
 
-// Diagnostic (not part of the stable ABI): 0 sends n0 = 4 decodes back to the lane-per-trellis kernel
+// Diagnostic (not part of the stable ABI; 2: the wave kernel at 512 / 1024 trellises too, 3: its tasks skipped,
+// a timing probe): 0 sends n0 = 4 decodes back to the lane-per-trellis kernel
 // k_sc_del instead of the wave-per-task kernel (sc_del_w4.hip); the A/B of DESIGN 3.2.  Decisions are
 // identical either way.  Returns the previous setting.
-extern "C" int pcub_sc_set_deletion_wave(int32_t on) { return g_wave4.exchange(on ? 1 : 0); }
+extern "C" int pcub_sc_set_deletion_wave(int32_t on) { return g_wave4.exchange(on < 0 ? 0 : on > 3 ? 3 : on); }
 
 extern "C" int pcub_sc_set_deletion_dense(int32_t on) {
     return g_dense.exchange(on ? 1 : 0);

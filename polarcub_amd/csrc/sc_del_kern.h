@@ -757,7 +757,7 @@ PCUB_DEL_TABLE(4)
 DelKern del_kernel_n4_wide(int tb);
 // 16-input trellises (n0 = 4) without ones, 64 .. 1024 trellises, decode: one wave a (trellis,
 // depth-3 node) task, the trellises in LDS (trellis_wave.h): sc_del_w4.hip
-DelKern del_kernel_w4(int tb);
+DelKern del_kernel_w4(int tb, int alt = 0);
 
 // Kernel tables, one per translation-unit group (decode without / with guard-band ones, export),
 // so the large n0 = 3, 4 instantiations compile in parallel.  T up to 256 (one workgroup) in

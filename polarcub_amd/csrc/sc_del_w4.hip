@@ -107,8 +107,8 @@ __device__ __forceinline__ int w4_info(const DelArgs& A, int kk, const unsigned 
     return total;
 }
 
-template <int TB>
-__global__ __launch_bounds__(kDelBlock) void k_sc_del_w4(DelArgs A) {
+template <int TB, int MINB>
+__global__ __launch_bounds__(kDelBlock, MINB) void k_sc_del_w4(DelArgs A) {
     constexpr int T = 1 << TB;
     constexpr int LV = T / 16, NW = T / 64;
     constexpr int WPC = T / 2;  // x_hat words a codeword (16 T bits)
@@ -122,6 +122,8 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del_w4(DelArgs A) {
     __shared__ long long s_next;
     extern __shared__ uint32_t rxb[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // this workgroup's trellis caches (the launcher's workspace, kW4Cache bytes a trellis), or none
+    uint8_t* cache = A.leaf ? reinterpret_cast<uint8_t*>(A.leaf) + (size_t)blockIdx.x * T * kW4Cache : nullptr;
     for (long long it = 0;; ++it) {
         long long cw;
         if (A.wtiles) {
@@ -153,15 +155,26 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del_w4(DelArgs A) {
         }
         __syncthreads();
         int ib = 0;  // information bits so far
+        int have1 = -1, have2 = -1;  // the depth-1 (k >> 2) / depth-2 (k >> 1) trellises in the cache
 #pragma unroll 1
         for (int k = 0; k < 8; ++k) {
             const int km = 2 * k, kp = 2 * k + 1;
-            if (!(w4_rate0<T>(A.fmask, km) && w4_rate0<T>(A.fmask, kp))) {
+            // (A.gate_id bit 0, diagnostics only: skip the tasks, so a launch times the rest)
+            if (!(A.gate_id & 1ull) && !(w4_rate0<T>(A.fmask, km) && w4_rate0<T>(A.fmask, kp))) {
+                int mode = 0;
+                if (cache) {
+                    mode = have2 == (k >> 1) ? kW4Load2 : ((have1 == (k >> 2) ? kW4Load1 : kW4Save1) | kW4Save2);
+                    if (mode & kW4Save1) have1 = k >> 2;
+                    have2 = k >> 1;
+                }
 #pragma unroll 1
                 for (int t = wv; t < T; t += kW4Waves) {
+                    // the task's segment and history are wave-uniform: scalar registers
                     W4Dims D;
-                    D.set(sm[t], sy[t], A.pd);
-                    w4_task(W4WaveRun{lane}, wb[wv], D, k, hist[t]);
+                    D.set(__builtin_amdgcn_readfirstlane((int)sm[t]), (uint32_t)__builtin_amdgcn_readfirstlane((int)sy[t]),
+                          A.pd);
+                    w4_task(W4WaveRun{lane}, wb[wv], D, k, (uint32_t)__builtin_amdgcn_readfirstlane((int)hist[t]),
+                            cache ? cache + (size_t)t * kW4Cache : nullptr, mode);
                     if (lane < 3) {
                         const int p = (int)bitrev((uint32_t)t, TB);
                         double* dst = lane == 0 ? vm : lane == 1 ? vp0 : vp1;
@@ -200,13 +213,14 @@ __global__ __launch_bounds__(kDelBlock) void k_sc_del_w4(DelArgs A) {
 
 }  // namespace
 
-DelKern del_kernel_w4(int tb) {
+DelKern del_kernel_w4(int tb, int alt) {
+    (void)alt;
     switch (tb) {
-        case 6: return k_sc_del_w4<6>;
-        case 7: return k_sc_del_w4<7>;
-        case 8: return k_sc_del_w4<8>;
-        case 9: return k_sc_del_w4<9>;
-        case 10: return k_sc_del_w4<10>;
+        case 6: return k_sc_del_w4<6, 1>;
+        case 7: return k_sc_del_w4<7, 1>;
+        case 8: return k_sc_del_w4<8, 1>;
+        case 9: return k_sc_del_w4<9, 1>;
+        case 10: return k_sc_del_w4<10, 1>;
         default: return nullptr;
     }
 }

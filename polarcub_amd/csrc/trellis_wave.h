@@ -48,6 +48,11 @@ constexpr uint32_t kW4None = 0xffffffffu;
 constexpr uint8_t kW4NoC = 0xffu;
 constexpr uint16_t kW4NoV = 0xffffu;
 
+// n / d for n < 2^16, 0 < d < 512 by one multiply (exhaustively checked on the host): the phases
+// decode their flat item indices without integer division
+PCUB_HD uint32_t w4_magic(int d) { return (1u << 25) / (uint32_t)d + 1u; }
+PCUB_HD int w4_div(int n, uint32_t mg) { return (int)(((uint64_t)(uint32_t)n * mg) >> 25); }
+
 // a segment: m received symbols (m <= 16), bits y, the channel's edge probabilities
 struct W4Dims {
     int m, dd, pw;
@@ -267,53 +272,117 @@ PCUB_HD void w4_item(const W4Dims& D, int d, const W4View& P, const W4View& C, i
 }
 
 // ---- the phases (lane-strided loops; a wave barrier between consecutive phases) ----
+//
+// Enumeration.  Of a depth-d layer j's pw x na(d) (from, advance) slot pairs only those with the
+// from-position in the layer's window [lo(j 2^d), hi(j 2^d)] (nu of them) and the to-position in the
+// next layer's window can hold an edge: w4_arange gives each from-position's advance offsets, at most
+// K = min(na, nu(next)) of them.  Every phase walks only these pairs (the other slots are never
+// written, so never read): the end layers, whose windows are single positions, hold ~1/9 of their
+// dense slots at n0 = 4.
+
+// advance offsets [a0, a1] of window offset uo in depth-d layer j
+PCUB_HD void w4_arange(const W4Dims& D, int d, int j, int uo, int& a0, int& a1) {
+    const int u = D.lo(j << d) + uo, AM = D.amin(d), NA = D.na(d);
+    const int b1 = (j + 1) << d;
+    a0 = D.lo(b1) - u - AM;
+    a0 = a0 > 0 ? a0 : 0;
+    a1 = D.hi(b1) - u - AM;
+    a1 = a1 < NA - 1 ? a1 : NA - 1;
+}
+
+PCUB_HD int w4_nu(const W4Dims& D, int b) { return D.hi(b) - D.lo(b) + 1; }
+
+// the enumerated pairs of a depth-d trellis: layer j holds nu(j) x K(j) items (from offset, k-th
+// advance offset of it); returns the total
+PCUB_HD int w4_items(const W4Dims& D, int d) {
+    const int LEN = kW4L >> d, NA = D.na(d);
+    int n = 0;
+    for (int j = 0; j < LEN; ++j) {
+        const int nn = w4_nu(D, (j + 1) << d);
+        n += w4_nu(D, j << d) * (NA < nn ? NA : nn);
+    }
+    return n;
+}
+
+// item i -> (layer j, from offset uo, advance offset ao); false when that advance falls outside the
+// next window (a from-position near a window end has fewer than K)
+PCUB_HD bool w4_item_of(const W4Dims& D, int d, int i, int& j, int& uo, int& ao) {
+    const int LEN = kW4L >> d, NA = D.na(d);
+    int off = 0;
+    for (int jj = 0; jj < LEN; ++jj) {
+        const int nn = w4_nu(D, (jj + 1) << d);
+        const int K = NA < nn ? NA : nn;
+        const int cnt = w4_nu(D, jj << d) * K;
+        if (i < off + cnt) {
+            const int r = i - off;
+            uo = w4_div(r, w4_magic(K));
+            j = jj;
+            int a0, a1;
+            w4_arange(D, d, jj, uo, a0, a1);
+            ao = a0 + (r - uo * K);
+            return ao <= a1;
+        }
+        off += cnt;
+    }
+    return false;
+}
 
 // child edges of the transform into depth d + 1 (d = 0: from the base)
 PCUB_HD void w4_ph_edges(const W4Dims& D, int d, const W4View& P, const W4View& C, uint32_t dec, bool plus,
                          int lane) {
-    const int LEN = kW4L >> (d + 1);
-    const int NA = D.na(d + 1);
-    const int per = D.pw * NA;
-    for (int i = lane; i < LEN * per; i += 64) {
-        const int j = i / per, r = i - j * per;
-        const int uo = r / NA, ao = r - uo * NA;
+    const int n = w4_items(D, d + 1);
+    for (int i = lane; i < n; i += 64) {
+        int j, uo, ao;
+        if (!w4_item_of(D, d + 1, i, j, uo, ao)) continue;
         const int dj = (int)((dec >> j) & 1u);
         if (d == 0) w4_base_item(D, C, j, uo, ao, dj, plus);
         else w4_item(D, d, P, C, j, uo, ao, dj, plus);
     }
 }
 
-// creation ranks of the child's edges; zero the normalisation counters
+// creation ranks of the child's edges (both labels of a pair against the layer's enumerated keys);
+// zero the normalisation counters
 PCUB_HD void w4_ph_rank(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
-    const int LEN = kW4L >> dc, SL = D.sl(dc);
-    for (int s = lane; s < LEN * SL; s += 64) {
-        const uint32_t k = C.k[s];
-        uint8_t c = kW4NoC;
-        if (k != kW4None) {
-            const int j = s / SL;
-            int n = 0;
-            for (int t = j * SL; t < (j + 1) * SL; ++t) n += C.k[t] < k ? 1 : 0;
-            c = (uint8_t)n;
+    const int SL = D.sl(dc), NA = D.na(dc);
+    const int n = w4_items(D, dc);
+    for (int i = lane; i < n; i += 64) {
+        int j, uo, ao;
+        if (!w4_item_of(D, dc, i, j, uo, ao)) continue;
+        const int s = j * SL + (uo * NA + ao) * 2;
+        const uint32_t k0 = C.k[s], k1 = C.k[s + 1];
+        int n0 = 0, n1 = 0;
+        const int nu = w4_nu(D, j << dc);
+        for (int uo2 = 0; uo2 < nu; ++uo2) {
+            int a0, a1;
+            w4_arange(D, dc, j, uo2, a0, a1);
+            const uint2* kl = reinterpret_cast<const uint2*>(C.k + j * SL + uo2 * NA * 2);
+            for (int ao2 = a0; ao2 <= a1; ++ao2) {
+                const uint2 q = kl[ao2];
+                n0 += (q.x < k0 ? 1 : 0) + (q.y < k0 ? 1 : 0);
+                n1 += (q.x < k1 ? 1 : 0) + (q.y < k1 ? 1 : 0);
+            }
         }
-        C.c[s] = c;
+        C.c[s] = k0 == kW4None ? kW4NoC : (uint8_t)n0;
+        C.c[s + 1] = k1 == kW4None ? kW4NoC : (uint8_t)n1;
     }
     if (lane < 16) b.ncnt[lane >> 1][lane & 1] = 0u;
 }
 
-// vertex keys of the child's layers 1 .. LEN-1 (D3: layer 1 only); zero the normalisation scratch
+// vertex keys of the child's layers 1 .. LEN-1 (D3: layer 1 only)
 PCUB_HD void w4_ph_vkey(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
     const int LEN = kW4L >> dc, SL = D.sl(dc), NA = D.na(dc), AM = D.amin(dc);
     const int nl = LEN - 1;
+    const uint32_t mpw = w4_magic(D.pw);
     for (int i = lane; i < nl * D.pw; i += 64) {
-        const int l = 1 + i / D.pw, po = i % D.pw;
+        const int l = 1 + w4_div(i, mpw), po = i - (l - 1) * D.pw;
         const int p = D.lo(l << dc) + po;
         uint16_t vk = kW4NoV;
         if (p <= D.hi(l << dc)) {
             int k0 = 0xffff;
-            const int plo = D.lo((l - 1) << dc);
+            const int plo = D.lo((l - 1) << dc), pnu = w4_nu(D, (l - 1) << dc);
             for (int ao = 0; ao < NA; ++ao) {
                 const int uo = p - AM - ao - plo;
-                if (uo < 0 || uo >= D.pw) continue;
+                if (uo < 0 || uo >= pnu) continue;
                 const int s = (l - 1) * SL + (uo * NA + ao) * 2;
                 for (int x = 0; x < 2; ++x) {
                     const int c = C.c[s + x];
@@ -323,26 +392,27 @@ PCUB_HD void w4_ph_vkey(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int 
             if (k0 != 0xffff) {
                 vk = (uint16_t)k0;
             } else {
-                int k1 = 0xffff;
-                for (int t = 0; t < NA * 2; ++t) {
-                    const int c = C.c[l * SL + po * NA * 2 + t];
-                    if (c != kW4NoC && c < k1) k1 = c;
-                }
+                int k1 = 0xffff, a0, a1;
+                w4_arange(D, dc, l, po, a0, a1);
+                for (int ao = a0; ao <= a1; ++ao)
+                    for (int x = 0; x < 2; ++x) {
+                        const int c = C.c[l * SL + (po * NA + ao) * 2 + x];
+                        if (c != kW4NoC && c < k1) k1 = c;
+                    }
                 if (k1 != 0xffff) vk = (uint16_t)(256 + k1);
             }
         }
         b.vkey[l - 1][po] = vk;
     }
-    const int total = LEN * SL;
-    for (int i = lane; i < total; i += 64) C.tmp[i] = 0.0;
 }
 
 // vertex insertion ranks from the keys (layer 0: the start vertex alone)
 PCUB_HD void w4_ph_vrank(const W4Dims& D, int dc, const W4View& C, const W4Buf& b, int lane) {
     const int LEN = kW4L >> dc;
     const int nl = LEN - 1;
+    const uint32_t mpw = w4_magic(D.pw);
     for (int i = lane; i < nl * D.pw; i += 64) {
-        const int l = 1 + i / D.pw, po = i % D.pw;
+        const int l = 1 + w4_div(i, mpw), po = i - (l - 1) * D.pw;
         const uint16_t vk = b.vkey[l - 1][po];
         int r = 0, nv = 0;
         for (int t = 0; t < D.pw; ++t) {
@@ -358,41 +428,59 @@ PCUB_HD void w4_ph_vrank(const W4Dims& D, int dc, const W4View& C, const W4Buf& 
         }
         if (po == 0) C.nv[l] = (uint8_t)nv;
     }
+    if (lane < kW4PW) C.vr[0][lane] = lane == 0 ? 0 : kW4NoC;
     if (lane == 0) {
-        C.vr[0][0] = 0;
         C.vo[0][0] = 0;
         C.nv[0] = 1;
     }
 }
 
-// normalisation order: each edge's position among its layer's same-label edges by
-// (from-vertex rank, creation rank), its probability scattered there
+// normalisation order: each edge's position among its layer's same-label edges by (from-vertex rank,
+// creation rank), its probability scattered there.  Items (layer, from-vertex, label): the edges of
+// the vertices ranked before it, then its own by creation rank.
 PCUB_HD void w4_ph_norder(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
     const int LEN = kW4L >> dc, SL = D.sl(dc), NA = D.na(dc);
-    const int half = SL / 2;
-    for (int s = lane; s < LEN * SL; s += 64) {
-        const int c = C.c[s];
-        if (c == kW4NoC) continue;
-        const int j = s / SL, r = s - j * SL, x = r & 1;
-        const int key = (C.vr[j][(r >> 1) / NA] << 8) | c;
-        int n = 0;
-        for (int t = x; t < SL; t += 2) {
-            const int c2 = C.c[j * SL + t];
-            if (c2 == kW4NoC) continue;
-            const int k2 = (C.vr[j][(t >> 1) / NA] << 8) | c2;
-            n += k2 < key ? 1 : 0;
+    const int half = SL / 2, pw = D.pw;
+    const uint32_t mper = w4_magic(2 * pw);
+    for (int i = lane; i < LEN * pw * 2; i += 64) {
+        const int j = w4_div(i, mper), r = i - j * 2 * pw;
+        const int uo = r >> 1, x = r & 1;
+        const int nu = w4_nu(D, j << dc);
+        if (uo >= nu) continue;
+        const int vr = C.vr[j][uo];
+        if (vr == kW4NoC) continue;
+        const uint8_t* cl = C.c + j * SL + x;  // label-x slot (uo2, ao2) at cl[2 (uo2 NA + ao2)]
+        int base = 0;
+        for (int uo2 = 0; uo2 < nu; ++uo2) {
+            if (C.vr[j][uo2] >= vr) continue;  // absent vertices (kW4NoC) rank after every present one
+            int a0, a1;
+            w4_arange(D, dc, j, uo2, a0, a1);
+            for (int ao2 = a0; ao2 <= a1; ++ao2) base += cl[2 * (uo2 * NA + ao2)] != kW4NoC ? 1 : 0;
         }
-        C.tmp[j * SL + x * half + n] = C.p[s];
+        int a0, a1;
+        w4_arange(D, dc, j, uo, a0, a1);
+        const uint8_t* own = cl + 2 * uo * NA;
+        int cnt = 0;
+        for (int ao = a0; ao <= a1; ++ao) {
+            const int c = own[2 * ao];
+            if (c == kW4NoC) continue;
+            ++cnt;
+            int n = base;
+            for (int ao2 = a0; ao2 <= a1; ++ao2) n += own[2 * ao2] < c ? 1 : 0;
+            C.tmp[j * SL + x * half + n] = C.p[j * SL + 2 * (uo * NA + ao) + x];
+        }
+        if (cnt) {
 #if defined(__HIP_DEVICE_COMPILE__)
-        atomicAdd(&b.ncnt[j][x], 1u);
+            atomicAdd(&b.ncnt[j][x], (uint32_t)cnt);
 #else
-        ++b.ncnt[j][x];
+            b.ncnt[j][x] += (uint32_t)cnt;
 #endif
+        }
     }
 }
 
-// the per-(layer, label) sums, each by one lane in order (4 terms a step: the zeros after the last
-// term change nothing)
+// the per-(layer, label) sums, each by one lane in order, four terms a step (terms past the count
+// read as 0.0, which changes no sum here: every sum is of non-negative terms from +0.0)
 PCUB_HD void w4_ph_nsum(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
     const int LEN = kW4L >> dc, SL = D.sl(dc);
     if (lane < 2 * LEN) {
@@ -401,8 +489,8 @@ PCUB_HD void w4_ph_nsum(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int 
         const int n = (int)b.ncnt[j][x];
         double s = 0.0;
         for (int i = 0; i < n; i += 4) {
-            const double t0 = t[i], t1 = i + 1 < SL / 2 ? t[i + 1] : 0.0, t2 = i + 2 < SL / 2 ? t[i + 2] : 0.0,
-                         t3 = i + 3 < SL / 2 ? t[i + 3] : 0.0;
+            const double t0 = t[i], t1 = i + 1 < n ? t[i + 1] : 0.0, t2 = i + 2 < n ? t[i + 2] : 0.0,
+                         t3 = i + 3 < n ? t[i + 3] : 0.0;
             s += t0;
             s += t1;
             s += t2;
@@ -414,14 +502,17 @@ PCUB_HD void w4_ph_nsum(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int 
 
 // normalize: every edge of layer j divided by max(s0, s1) (1 when both are 0)
 PCUB_HD void w4_ph_ndiv(const W4Dims& D, int dc, const W4View& C, const W4Buf& b, int lane) {
-    const int LEN = kW4L >> dc, SL = D.sl(dc);
-    for (int s = lane; s < LEN * SL; s += 64) {
-        if (C.c[s] == kW4NoC) continue;
-        const int j = s / SL;
+    const int SL = D.sl(dc), NA = D.na(dc);
+    const int n = w4_items(D, dc);
+    for (int i = lane; i < n; i += 64) {
+        int j, uo, ao;
+        if (!w4_item_of(D, dc, i, j, uo, ao)) continue;
+        const int s = j * SL + (uo * NA + ao) * 2;
         const double s0 = b.sums[j][0], s1 = b.sums[j][1];
         double dv = s0 >= s1 ? s0 : s1;
         if (dv == 0.0) dv = 1.0;
-        C.p[s] = C.p[s] / dv;
+        for (int x = 0; x < 2; ++x)
+            if (C.c[s + x] != kW4NoC) C.p[s + x] = C.p[s + x] / dv;
     }
 }
 
@@ -463,6 +554,42 @@ PCUB_HD void w4_ph_collapse(const W4Dims& D, const W4View& C, W4Buf& b, int lane
     b.out[lane] = norm_pack(m0, m1);
 }
 
+// ---- the per-trellis cache of the depth-1 and depth-2 trellises ----
+//
+// Node k's depth-1 trellis depends only on k >> 2 (minus for k < 4, the plus child under the first
+// four nodes' decisions after), its depth-2 trellis only on k >> 1: the kernel keeps the last of each
+// per trellis in global memory (kW4Cache bytes a trellis) and reloads instead of rebuilding -- what the
+// next transform reads: probabilities, creation ranks, middle-layer vertex orders.
+constexpr int kW4C1 = 4096;  // depth 1: p[432] doubles, c[432], vo[9][9], nv[9]
+constexpr int kW4C2 = 3328;  // depth 2: p[360] doubles, c[360], vo[5][9], nv[5]
+constexpr int kW4Cache = kW4C1 + kW4C2;
+enum { kW4Load1 = 1, kW4Save1 = 2, kW4Load2 = 4, kW4Save2 = 8 };
+
+PCUB_HD void w4_cache_io(const W4Dims& D, int d, const W4View& V, uint8_t* g, bool save, int lane) {
+    const int LEN = kW4L >> d, n = LEN * D.sl(d);
+    const int cap = d == 1 ? kW4SA : kW4SB;
+    double* gp = reinterpret_cast<double*>(g);
+    uint8_t* gc = g + cap * 8;
+    uint8_t* gv = gc + cap;
+    uint8_t* vo = &V.vo[0][0];
+    const int nvo = (LEN + 1) * kW4PW;
+    if (save) {
+        for (int i = lane; i < n; i += 64) {
+            gp[i] = V.p[i];
+            gc[i] = V.c[i];
+        }
+        for (int i = lane; i < nvo; i += 64) gv[i] = vo[i];
+        if (lane <= LEN) gv[nvo + lane] = V.nv[lane];
+    } else {
+        for (int i = lane; i < n; i += 64) {
+            V.p[i] = gp[i];
+            V.c[i] = gc[i];
+        }
+        for (int i = lane; i < nvo; i += 64) vo[i] = gv[i];
+        if (lane <= LEN) V.nv[lane] = gv[nvo + lane];
+    }
+}
+
 // The re-encoding of a node's returned bits: x[2h] = ym[h] ^ yp[h], x[2h+1] = yp[h] (DelNode)
 PCUB_HD uint32_t w4_combine(uint32_t ym, uint32_t yp, int H) {
     uint32_t x = 0;
@@ -480,38 +607,56 @@ PCUB_HD uint32_t w4_enc16(uint32_t hist) { return w4_combine(w4_enc8(hist, 0), w
 
 // One task: depth-3 node k of a segment with decision history hist (bit 2i / 2i+1: the minus / plus
 // subtree of node i < k).  `run(f)` runs f(lane) on every lane of the wave, then a wave barrier.
-// Leaves b.out[0..2] = the minus row, the plus row after decision 0, after decision 1.
+// With a cache (kW4Cache bytes, this trellis's), `mode` loads the depth-1 / depth-2 trellis from it
+// instead of building it (kW4Load1 / kW4Load2: the caller knows it holds node k's) or saves the built
+// one (kW4Save1 / kW4Save2).  Leaves b.out[0..2] = the minus row, the plus row after decision 0, after 1.
 template <class Run>
-PCUB_HD void w4_task(const Run& run, W4Buf& b, const W4Dims& D, int k, uint32_t hist) {
+PCUB_HD void w4_task(const Run& run, W4Buf& b, const W4Dims& D, int k, uint32_t hist, uint8_t* cache = nullptr,
+                     int mode = 0) {
     if (D.m > kW4L) {  // no edges (BaseT with m > L): every row is the collapse of an empty trellis
         run([&](int lane) {
             if (lane < 3) b.out[lane] = norm_pack(0.0, 0.0);
         });
         return;
     }
+    if (!cache) mode = 0;
     const W4View A = w4_view_a(b), B = w4_view_b(b);
     const bool p1 = (k >> 2) & 1, p2 = (k >> 1) & 1, p3 = k & 1;
     const uint32_t d1 = p1 ? w4_enc8(hist, 0) : 0u;
     const uint32_t d2 = p2 ? w4_enc4(hist, (k >> 1) - 1) : 0u;
     const uint32_t d3 = p3 ? w4_enc2(hist, k - 1) : 0u;
-    // depth 1 (region A) from the base
-    run([&](int lane) { w4_ph_edges(D, 0, A, A, d1, p1, lane); });
-    run([&](int lane) { w4_ph_rank(D, 1, A, b, lane); });
-    run([&](int lane) { w4_ph_vkey(D, 1, A, b, lane); });
-    run([&](int lane) { w4_ph_vrank(D, 1, A, b, lane); });
-    run([&](int lane) { w4_ph_norder(D, 1, A, b, lane); });
-    run([&](int lane) { w4_ph_nsum(D, 1, A, b, lane); });
-    run([&](int lane) { w4_ph_ndiv(D, 1, A, b, lane); });
-    // depth 2 (region B)
-    run([&](int lane) { w4_ph_edges(D, 1, A, B, d2, p2, lane); });
-    run([&](int lane) { w4_ph_rank(D, 2, B, b, lane); });
-    run([&](int lane) { w4_ph_vkey(D, 2, B, b, lane); });
-    run([&](int lane) { w4_ph_vrank(D, 2, B, b, lane); });
-    run([&](int lane) { w4_ph_norder(D, 2, B, b, lane); });
-    run([&](int lane) { w4_ph_nsum(D, 2, B, b, lane); });
-    run([&](int lane) { w4_ph_ndiv(D, 2, B, b, lane); });
+    if (!(mode & kW4Load2)) {
+        // depth 1 (region A) from the base, or from the cache
+        if (mode & kW4Load1) {
+            run([&](int lane) { w4_cache_io(D, 1, A, cache, false, lane); });
+        } else {
+            run([&](int lane) { w4_ph_edges(D, 0, A, A, d1, p1, lane); });
+            run([&](int lane) { w4_ph_rank(D, 1, A, b, lane); });
+            run([&](int lane) { w4_ph_vkey(D, 1, A, b, lane); });
+            run([&](int lane) { w4_ph_vrank(D, 1, A, b, lane); });
+            run([&](int lane) { w4_ph_norder(D, 1, A, b, lane); });
+            run([&](int lane) { w4_ph_nsum(D, 1, A, b, lane); });
+            run([&](int lane) { w4_ph_ndiv(D, 1, A, b, lane); });
+        }
+        // depth 2 (region B)
+        run([&](int lane) {
+            if (mode & kW4Save1) w4_cache_io(D, 1, A, cache, true, lane);
+            w4_ph_edges(D, 1, A, B, d2, p2, lane);
+        });
+        run([&](int lane) { w4_ph_rank(D, 2, B, b, lane); });
+        run([&](int lane) { w4_ph_vkey(D, 2, B, b, lane); });
+        run([&](int lane) { w4_ph_vrank(D, 2, B, b, lane); });
+        run([&](int lane) { w4_ph_norder(D, 2, B, b, lane); });
+        run([&](int lane) { w4_ph_nsum(D, 2, B, b, lane); });
+        run([&](int lane) { w4_ph_ndiv(D, 2, B, b, lane); });
+    } else {
+        run([&](int lane) { w4_cache_io(D, 2, B, cache + kW4C1, false, lane); });
+    }
     // depth 3 (region A again)
-    run([&](int lane) { w4_ph_edges(D, 2, B, A, d3, p3, lane); });
+    run([&](int lane) {
+        if (mode & kW4Save2) w4_cache_io(D, 2, B, cache + kW4C1, true, lane);
+        w4_ph_edges(D, 2, B, A, d3, p3, lane);
+    });
     run([&](int lane) { w4_ph_rank(D, 3, A, b, lane); });
     run([&](int lane) { w4_ph_vkey(D, 3, A, b, lane); });
     run([&](int lane) { w4_ph_vrank(D, 3, A, b, lane); });

@@ -67,6 +67,7 @@ int main(int argc, char** argv) {
     std::mt19937_64 rng(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1);
     const double pds[] = {0.0, 0.01, 0.1, 0.1, 0.2, 0.37, 0.5, 0.9, 1.0};
     auto* wb = new W4Buf;
+    auto* cache = new uint8_t[kW4Cache];
     long long hist_m[18] = {};
     for (long long i = 0; i < n; ++i) {
         const int r = (int)(rng() % 16);
@@ -85,8 +86,20 @@ int main(int argc, char** argv) {
         const uint32_t xr = ref_rows(b, hist, rows);
         W4Dims D;
         D.set(m, y, pd);
+        // half the cases run through the depth-1 / depth-2 cache as sc_del_w4.hip drives it, with random
+        // nodes skipped (rate-0 nodes run no tasks, so a later node may find its trellis not cached)
+        const bool use_cache = (i & 1) != 0;
+        const uint32_t skip = use_cache ? (uint32_t)(rng() & rng() & 0xffu) : 0u;
+        int have1 = -1, have2 = -1;
         for (int k = 0; k < 8; ++k) {
-            w4_task(HostRun{}, *wb, D, k, hist);
+            if ((skip >> k) & 1u) continue;
+            int mode = 0;
+            if (use_cache) {
+                mode = (have2 == (k >> 1)) ? kW4Load2 : ((have1 == (k >> 2)) ? kW4Load1 : kW4Save1) | kW4Save2;
+                if (mode & kW4Save1) have1 = k >> 2;
+                have2 = k >> 1;
+            }
+            w4_task(HostRun{}, *wb, D, k, hist, use_cache ? cache : nullptr, mode);
             for (int o = 0; o < 3; ++o) {
                 ++g_cmp;
                 if (!same_bits(wb->out[o], rows[k][o])) {
@@ -100,6 +113,7 @@ int main(int argc, char** argv) {
         if (w4_enc16(hist) != xr && g_fail++ < 12) std::printf("case %lld: encoding %#x vs %#x\n", i, w4_enc16(hist), xr);
     }
     delete wb;
+    delete[] cache;
     std::printf("w4_check: %lld cases, %lld comparisons, %lld mismatches; m histogram:", n, g_cmp, g_fail);
     for (int m = 0; m < 18; ++m) std::printf(" %lld", hist_m[m]);
     std::printf("\n");

@@ -150,7 +150,7 @@ def test_wave_kernel_matches_lane_kernel(sc, n):
         for i, w in enumerate(words):
             rx[i, :len(w)] = w
         ln = np.array([len(w) for w in words], np.int32)
-        old = sc.set_deletion_wave(1)
+        old = sc.set_deletion_wave(2)  # the wave kernel at every size
         try:
             info_w, xhat_w = _dec(sc, n, n0, pd, frozen, fval, rx, ln)
             sc.set_deletion_wave(0)

@@ -217,10 +217,10 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     const long long rw = ((long long)stride + 31) / 32;
     // n0 = 4 without ones (main_deletion's n = 12 .. 14): one wave a (trellis, depth-3 node) task, the
     // trellises in LDS (sc_del_w4.hip), codewords from a per-launch counter
-    // (at 512 / 1024 trellises, n = 13 / 14, the lane kernel is still faster: 16.8 / 9.9 k against 11.7 / 5.8 k
-    // cw/s; the wave kernel takes them when asked, pcub_sc_set_deletion_wave(2))
+    // (at 1024 trellises, n = 14, the lane kernel is still faster: 10.0 k against 6.1 k cw/s -- the wave
+    // kernel's 64-value memoryless subtree spills; it takes them when asked, pcub_sc_set_deletion_wave(2))
     const int w4m = g_wave4.load(std::memory_order_relaxed);
-    if (!exp && n0 == 4 && ones == 0 && w4m && (n - n0 <= 8 || w4m == 2) && rw * 4 <= kW4MaxRxLds) {
+    if (!exp && n0 == 4 && ones == 0 && w4m && (n - n0 <= 9 || w4m == 2) && rw * 4 <= kW4MaxRxLds) {
         const DelKern wk = del_kernel_w4(n - n0, 0);
         if (wk) {
             A.rw = (int)rw;

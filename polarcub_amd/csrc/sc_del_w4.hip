@@ -214,13 +214,15 @@ __global__ __launch_bounds__(kDelBlock, MINB) void k_sc_del_w4(DelArgs A) {
 }  // namespace
 
 DelKern del_kernel_w4(int tb, int alt) {
+    // two workgroups a CU (eight waves): the register allocator must fit the memoryless subtree and the
+    // task phases into 256 VGPRs; unbounded, the subtree's register tree pushed TB = 8 to one wave a SIMD
     (void)alt;
     switch (tb) {
-        case 6: return k_sc_del_w4<6, 1>;
-        case 7: return k_sc_del_w4<7, 1>;
-        case 8: return k_sc_del_w4<8, 1>;
-        case 9: return k_sc_del_w4<9, 1>;
-        case 10: return k_sc_del_w4<10, 1>;
+        case 6: return k_sc_del_w4<6, 2>;
+        case 7: return k_sc_del_w4<7, 2>;
+        case 8: return k_sc_del_w4<8, 2>;
+        case 9: return k_sc_del_w4<9, 2>;
+        case 10: return k_sc_del_w4<10, 2>;
         default: return nullptr;
     }
 }

@@ -46,7 +46,7 @@ constexpr int kW4SA = 432;    // region A: depth 1 (8 x 9 x 3 x 2) or depth 3 (2
 constexpr int kW4SB = 360;    // region B: depth 2 (4 x 9 x 5 x 2)
 constexpr uint32_t kW4None = 0xffffffffu;
 constexpr uint8_t kW4NoC = 0xffu;
-constexpr uint16_t kW4NoV = 0xffffu;
+constexpr uint32_t kW4NoV = 0xffffffffu;
 
 // n / d for n < 2^16, 0 < d < 512 by one multiply (exhaustively checked on the host): the phases
 // decode their flat item indices without integer division
@@ -101,7 +101,7 @@ struct W4Dims {
 };
 
 // one wave's trellises (LDS on the device)
-struct W4Buf {
+struct alignas(16) W4Buf {
     double pA[kW4SA];        // region A: depth 1, later depth 3 (probabilities)
     uint32_t kA[kW4SA];      // ... first-contribution keys
     double pB[kW4SB];        // region B: depth 2
@@ -114,7 +114,7 @@ struct W4Buf {
     uint8_t vrB[5][kW4PW];
     uint8_t voB[5][kW4PW];
     uint8_t nvB[5];
-    uint16_t vkey[8][kW4PW];  // vertex keys of the layer being ranked
+    uint32_t vkey[8][kW4PW];  // vertex keys of the layer being ranked (phase << 31 | least edge key)
     uint32_t ncnt[8][2];      // edges a (layer, label) of the layer being normalised
     double sums[8][2];        // normalisation sums
     double out[3];            // the task's rows: minus, plus after 0, plus after 1
@@ -241,14 +241,19 @@ PCUB_HD void w4_item(const W4Dims& D, int d, const W4View& P, const W4View& C, i
             if (a1 < 0 || a1 >= NAp || a2 < 0 || a2 >= NAp) continue;
             const int ia = (2 * j) * SLp + (uo * NAp + a1) * 2;
             const int ib = (2 * j + 1) * SLp + (wo * NAp + a2) * 2;
-            const int ca0 = P.c[ia], ca1 = P.c[ia + 1];
-            const int cb0 = P.c[ib], cb1 = P.c[ib + 1];
+            // both labels of a slot pair in one read each (pairs start at even slots: 2- and 16-byte aligned)
+            const uint32_t cap = *reinterpret_cast<const uint16_t*>(P.c + ia);
+            const uint32_t cbp = *reinterpret_cast<const uint16_t*>(P.c + ib);
+            const double2 pap = *reinterpret_cast<const double2*>(P.p + ia);
+            const double2 pbp = *reinterpret_cast<const double2*>(P.p + ib);
+            const int ca0 = (int)(cap & 0xffu), ca1 = (int)(cap >> 8);
+            const int cb0 = (int)(cbp & 0xffu), cb1 = (int)(cbp >> 8);
             const int f = (ca1 < ca0) ? 1 : 0;  // the in-edge created first (kW4NoC sorts last)
             for (int t = 0; t < 2; ++t) {
                 const int la = f ^ t;
                 const int ca = la ? ca1 : ca0;
                 if (ca == kW4NoC) continue;
-                const double pa = P.p[ia + la];
+                const double pa = la ? pap.y : pap.x;
                 for (int x = 0; x < 2; ++x) {
                     int lb;
                     if (plus) {
@@ -259,7 +264,7 @@ PCUB_HD void w4_item(const W4Dims& D, int d, const W4View& P, const W4View& C, i
                     }
                     const int cb = lb ? cb1 : cb0;
                     if (cb == kW4NoC) continue;
-                    acc[x] += pa * P.p[ib + lb];
+                    acc[x] += pa * (lb ? pbp.y : pbp.x);
                     if (key[x] == kW4None) key[x] = ((uint32_t)r << 16) | ((uint32_t)ca << 8) | (uint32_t)cb;
                 }
             }
@@ -292,67 +297,59 @@ PCUB_HD void w4_arange(const W4Dims& D, int d, int j, int uo, int& a0, int& a1) 
 
 PCUB_HD int w4_nu(const W4Dims& D, int b) { return D.hi(b) - D.lo(b) + 1; }
 
-// the enumerated pairs of a depth-d trellis: layer j holds nu(j) x K(j) items (from offset, k-th
-// advance offset of it); returns the total
-PCUB_HD int w4_items(const W4Dims& D, int d) {
-    const int LEN = kW4L >> d, NA = D.na(d);
-    int n = 0;
-    for (int j = 0; j < LEN; ++j) {
-        const int nn = w4_nu(D, (j + 1) << d);
-        n += w4_nu(D, j << d) * (NA < nn ? NA : nn);
-    }
-    return n;
-}
+// Lanes.  A depth-d trellis has LEN = 16 >> d layers; each layer gets LPL = 64 / LEN lanes (8, 16,
+// 32), lane = j * LPL + q, and its q-th, (q + LPL)-th, .. item: no lane decodes a flat index.
+PCUB_HD int w4_lpl_log(int d) { return 2 + d; }
 
-// item i -> (layer j, from offset uo, advance offset ao); false when that advance falls outside the
-// next window (a from-position near a window end has fewer than K)
-PCUB_HD bool w4_item_of(const W4Dims& D, int d, int i, int& j, int& uo, int& ao) {
-    const int LEN = kW4L >> d, NA = D.na(d);
-    int off = 0;
-    for (int jj = 0; jj < LEN; ++jj) {
-        const int nn = w4_nu(D, (jj + 1) << d);
-        const int K = NA < nn ? NA : nn;
-        const int cnt = w4_nu(D, jj << d) * K;
-        if (i < off + cnt) {
-            const int r = i - off;
-            uo = w4_div(r, w4_magic(K));
-            j = jj;
-            int a0, a1;
-            w4_arange(D, d, jj, uo, a0, a1);
-            ao = a0 + (r - uo * K);
-            return ao <= a1;
-        }
-        off += cnt;
+// layer j's enumerated pairs: item r -> (uo, ao); false past the from-position's advance range
+struct W4Layer {
+    int j, nu, K;
+    uint32_t mk;
+    PCUB_HD void set(const W4Dims& D, int d, int j_) {
+        j = j_;
+        nu = w4_nu(D, j << d);
+        const int nn = w4_nu(D, (j + 1) << d), NA = D.na(d);
+        K = NA < nn ? NA : nn;
+        mk = w4_magic(K);
     }
-    return false;
-}
+    PCUB_HD bool item(const W4Dims& D, int d, int r, int& uo, int& ao) const {
+        uo = w4_div(r, mk);
+        int a0, a1;
+        w4_arange(D, d, j, uo, a0, a1);
+        ao = a0 + (r - uo * K);
+        return ao <= a1;
+    }
+};
 
 // child edges of the transform into depth d + 1 (d = 0: from the base)
 PCUB_HD void w4_ph_edges(const W4Dims& D, int d, const W4View& P, const W4View& C, uint32_t dec, bool plus,
                          int lane) {
-    const int n = w4_items(D, d + 1);
-    for (int i = lane; i < n; i += 64) {
-        int j, uo, ao;
-        if (!w4_item_of(D, d + 1, i, j, uo, ao)) continue;
-        const int dj = (int)((dec >> j) & 1u);
-        if (d == 0) w4_base_item(D, C, j, uo, ao, dj, plus);
-        else w4_item(D, d, P, C, j, uo, ao, dj, plus);
+    const int dc = d + 1, lg = w4_lpl_log(dc);
+    W4Layer Ly;
+    Ly.set(D, dc, lane >> lg);
+    const int dj = (int)((dec >> Ly.j) & 1u);
+    for (int r = lane & ((1 << lg) - 1); r < Ly.nu * Ly.K; r += 1 << lg) {
+        int uo, ao;
+        if (!Ly.item(D, dc, r, uo, ao)) continue;
+        if (d == 0) w4_base_item(D, C, Ly.j, uo, ao, dj, plus);
+        else w4_item(D, d, P, C, Ly.j, uo, ao, dj, plus);
     }
 }
 
 // creation ranks of the child's edges (both labels of a pair against the layer's enumerated keys);
 // zero the normalisation counters
 PCUB_HD void w4_ph_rank(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
-    const int SL = D.sl(dc), NA = D.na(dc);
-    const int n = w4_items(D, dc);
-    for (int i = lane; i < n; i += 64) {
-        int j, uo, ao;
-        if (!w4_item_of(D, dc, i, j, uo, ao)) continue;
+    const int SL = D.sl(dc), NA = D.na(dc), lg = w4_lpl_log(dc);
+    W4Layer Ly;
+    Ly.set(D, dc, lane >> lg);
+    const int j = Ly.j;
+    for (int r = lane & ((1 << lg) - 1); r < Ly.nu * Ly.K; r += 1 << lg) {
+        int uo, ao;
+        if (!Ly.item(D, dc, r, uo, ao)) continue;
         const int s = j * SL + (uo * NA + ao) * 2;
         const uint32_t k0 = C.k[s], k1 = C.k[s + 1];
         int n0 = 0, n1 = 0;
-        const int nu = w4_nu(D, j << dc);
-        for (int uo2 = 0; uo2 < nu; ++uo2) {
+        for (int uo2 = 0; uo2 < Ly.nu; ++uo2) {
             int a0, a1;
             w4_arange(D, dc, j, uo2, a0, a1);
             const uint2* kl = reinterpret_cast<const uint2*>(C.k + j * SL + uo2 * NA * 2);
@@ -368,38 +365,38 @@ PCUB_HD void w4_ph_rank(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int 
     if (lane < 16) b.ncnt[lane >> 1][lane & 1] = 0u;
 }
 
-// vertex keys of the child's layers 1 .. LEN-1 (D3: layer 1 only)
+// vertex keys of the child's layers 1 .. LEN-1 (D3: layer 1 only), from the edge keys: a layer's
+// creation order is the order of its keys, so the least creation rank of a vertex's in- (out-) edges
+// is that of their least key.  Runs in the rank phase (it reads only keys).
 PCUB_HD void w4_ph_vkey(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
-    const int LEN = kW4L >> dc, SL = D.sl(dc), NA = D.na(dc), AM = D.amin(dc);
-    const int nl = LEN - 1;
-    const uint32_t mpw = w4_magic(D.pw);
-    for (int i = lane; i < nl * D.pw; i += 64) {
-        const int l = 1 + w4_div(i, mpw), po = i - (l - 1) * D.pw;
+    const int LEN = kW4L >> dc, SL = D.sl(dc), NA = D.na(dc), AM = D.amin(dc), lg = w4_lpl_log(dc);
+    const int l = lane >> lg;
+    if (l == 0 || l >= LEN) return;
+    for (int po = lane & ((1 << lg) - 1); po < D.pw; po += 1 << lg) {
         const int p = D.lo(l << dc) + po;
-        uint16_t vk = kW4NoV;
+        uint32_t vk = kW4NoV;
         if (p <= D.hi(l << dc)) {
-            int k0 = 0xffff;
+            uint32_t k0 = kW4None;
             const int plo = D.lo((l - 1) << dc), pnu = w4_nu(D, (l - 1) << dc);
             for (int ao = 0; ao < NA; ++ao) {
                 const int uo = p - AM - ao - plo;
                 if (uo < 0 || uo >= pnu) continue;
-                const int s = (l - 1) * SL + (uo * NA + ao) * 2;
-                for (int x = 0; x < 2; ++x) {
-                    const int c = C.c[s + x];
-                    if (c != kW4NoC && c < k0) k0 = c;
-                }
+                const uint2 q = *reinterpret_cast<const uint2*>(C.k + (l - 1) * SL + (uo * NA + ao) * 2);
+                k0 = q.x < k0 ? q.x : k0;
+                k0 = q.y < k0 ? q.y : k0;
             }
-            if (k0 != 0xffff) {
-                vk = (uint16_t)k0;
+            if (k0 != kW4None) {
+                vk = k0;
             } else {
-                int k1 = 0xffff, a0, a1;
+                uint32_t k1 = kW4None;
+                int a0, a1;
                 w4_arange(D, dc, l, po, a0, a1);
-                for (int ao = a0; ao <= a1; ++ao)
-                    for (int x = 0; x < 2; ++x) {
-                        const int c = C.c[l * SL + (po * NA + ao) * 2 + x];
-                        if (c != kW4NoC && c < k1) k1 = c;
-                    }
-                if (k1 != 0xffff) vk = (uint16_t)(256 + k1);
+                for (int ao = a0; ao <= a1; ++ao) {
+                    const uint2 q = *reinterpret_cast<const uint2*>(C.k + l * SL + (po * NA + ao) * 2);
+                    k1 = q.x < k1 ? q.x : k1;
+                    k1 = q.y < k1 ? q.y : k1;
+                }
+                if (k1 != kW4None) vk = 0x80000000u | k1;
             }
         }
         b.vkey[l - 1][po] = vk;
@@ -408,26 +405,25 @@ PCUB_HD void w4_ph_vkey(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int 
 
 // vertex insertion ranks from the keys (layer 0: the start vertex alone)
 PCUB_HD void w4_ph_vrank(const W4Dims& D, int dc, const W4View& C, const W4Buf& b, int lane) {
-    const int LEN = kW4L >> dc;
-    const int nl = LEN - 1;
-    const uint32_t mpw = w4_magic(D.pw);
-    for (int i = lane; i < nl * D.pw; i += 64) {
-        const int l = 1 + w4_div(i, mpw), po = i - (l - 1) * D.pw;
-        const uint16_t vk = b.vkey[l - 1][po];
-        int r = 0, nv = 0;
-        for (int t = 0; t < D.pw; ++t) {
-            const uint16_t o = b.vkey[l - 1][t];
-            r += o < vk ? 1 : 0;
-            nv += o != kW4NoV ? 1 : 0;
+    const int LEN = kW4L >> dc, lg = w4_lpl_log(dc);
+    const int l = lane >> lg;
+    if (l >= 1 && l < LEN)
+        for (int po = lane & ((1 << lg) - 1); po < D.pw; po += 1 << lg) {
+            const uint32_t vk = b.vkey[l - 1][po];
+            int r = 0, nv = 0;
+            for (int t = 0; t < D.pw; ++t) {
+                const uint32_t o = b.vkey[l - 1][t];
+                r += o < vk ? 1 : 0;
+                nv += o != kW4NoV ? 1 : 0;
+            }
+            if (vk != kW4NoV) {
+                C.vr[l][po] = (uint8_t)r;
+                C.vo[l][r] = (uint8_t)po;
+            } else {
+                C.vr[l][po] = kW4NoC;
+            }
+            if (po == 0) C.nv[l] = (uint8_t)nv;
         }
-        if (vk != kW4NoV) {
-            C.vr[l][po] = (uint8_t)r;
-            C.vo[l][r] = (uint8_t)po;
-        } else {
-            C.vr[l][po] = kW4NoC;
-        }
-        if (po == 0) C.nv[l] = (uint8_t)nv;
-    }
     if (lane < kW4PW) C.vr[0][lane] = lane == 0 ? 0 : kW4NoC;
     if (lane == 0) {
         C.vo[0][0] = 0;
@@ -436,17 +432,15 @@ PCUB_HD void w4_ph_vrank(const W4Dims& D, int dc, const W4View& C, const W4Buf& 
 }
 
 // normalisation order: each edge's position among its layer's same-label edges by (from-vertex rank,
-// creation rank), its probability scattered there.  Items (layer, from-vertex, label): the edges of
-// the vertices ranked before it, then its own by creation rank.
+// creation rank), its probability scattered there.  Items (from-vertex, label) of the lane's layer: the
+// edges of the vertices ranked before it, then its own by creation rank.
 PCUB_HD void w4_ph_norder(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int lane) {
-    const int LEN = kW4L >> dc, SL = D.sl(dc), NA = D.na(dc);
-    const int half = SL / 2, pw = D.pw;
-    const uint32_t mper = w4_magic(2 * pw);
-    for (int i = lane; i < LEN * pw * 2; i += 64) {
-        const int j = w4_div(i, mper), r = i - j * 2 * pw;
+    const int SL = D.sl(dc), NA = D.na(dc), lg = w4_lpl_log(dc);
+    const int half = SL / 2;
+    const int j = lane >> lg;
+    const int nu = w4_nu(D, j << dc);
+    for (int r = lane & ((1 << lg) - 1); r < 2 * nu; r += 1 << lg) {
         const int uo = r >> 1, x = r & 1;
-        const int nu = w4_nu(D, j << dc);
-        if (uo >= nu) continue;
         const int vr = C.vr[j][uo];
         if (vr == kW4NoC) continue;
         const uint8_t* cl = C.c + j * SL + x;  // label-x slot (uo2, ao2) at cl[2 (uo2 NA + ao2)]
@@ -502,15 +496,16 @@ PCUB_HD void w4_ph_nsum(const W4Dims& D, int dc, const W4View& C, W4Buf& b, int 
 
 // normalize: every edge of layer j divided by max(s0, s1) (1 when both are 0)
 PCUB_HD void w4_ph_ndiv(const W4Dims& D, int dc, const W4View& C, const W4Buf& b, int lane) {
-    const int SL = D.sl(dc), NA = D.na(dc);
-    const int n = w4_items(D, dc);
-    for (int i = lane; i < n; i += 64) {
-        int j, uo, ao;
-        if (!w4_item_of(D, dc, i, j, uo, ao)) continue;
-        const int s = j * SL + (uo * NA + ao) * 2;
-        const double s0 = b.sums[j][0], s1 = b.sums[j][1];
-        double dv = s0 >= s1 ? s0 : s1;
-        if (dv == 0.0) dv = 1.0;
+    const int SL = D.sl(dc), NA = D.na(dc), lg = w4_lpl_log(dc);
+    W4Layer Ly;
+    Ly.set(D, dc, lane >> lg);
+    const double s0 = b.sums[Ly.j][0], s1 = b.sums[Ly.j][1];
+    double dv = s0 >= s1 ? s0 : s1;
+    if (dv == 0.0) dv = 1.0;
+    for (int r = lane & ((1 << lg) - 1); r < Ly.nu * Ly.K; r += 1 << lg) {
+        int uo, ao;
+        if (!Ly.item(D, dc, r, uo, ao)) continue;
+        const int s = Ly.j * SL + (uo * NA + ao) * 2;
         for (int x = 0; x < 2; ++x)
             if (C.c[s + x] != kW4NoC) C.p[s + x] = C.p[s + x] / dv;
     }
@@ -631,8 +626,10 @@ PCUB_HD void w4_task(const Run& run, W4Buf& b, const W4Dims& D, int k, uint32_t 
             run([&](int lane) { w4_cache_io(D, 1, A, cache, false, lane); });
         } else {
             run([&](int lane) { w4_ph_edges(D, 0, A, A, d1, p1, lane); });
-            run([&](int lane) { w4_ph_rank(D, 1, A, b, lane); });
-            run([&](int lane) { w4_ph_vkey(D, 1, A, b, lane); });
+            run([&](int lane) {
+                w4_ph_rank(D, 1, A, b, lane);
+                w4_ph_vkey(D, 1, A, b, lane);
+            });
             run([&](int lane) { w4_ph_vrank(D, 1, A, b, lane); });
             run([&](int lane) { w4_ph_norder(D, 1, A, b, lane); });
             run([&](int lane) { w4_ph_nsum(D, 1, A, b, lane); });
@@ -643,8 +640,10 @@ PCUB_HD void w4_task(const Run& run, W4Buf& b, const W4Dims& D, int k, uint32_t 
             if (mode & kW4Save1) w4_cache_io(D, 1, A, cache, true, lane);
             w4_ph_edges(D, 1, A, B, d2, p2, lane);
         });
-        run([&](int lane) { w4_ph_rank(D, 2, B, b, lane); });
-        run([&](int lane) { w4_ph_vkey(D, 2, B, b, lane); });
+        run([&](int lane) {
+            w4_ph_rank(D, 2, B, b, lane);
+            w4_ph_vkey(D, 2, B, b, lane);
+        });
         run([&](int lane) { w4_ph_vrank(D, 2, B, b, lane); });
         run([&](int lane) { w4_ph_norder(D, 2, B, b, lane); });
         run([&](int lane) { w4_ph_nsum(D, 2, B, b, lane); });
@@ -657,8 +656,10 @@ PCUB_HD void w4_task(const Run& run, W4Buf& b, const W4Dims& D, int k, uint32_t 
         if (mode & kW4Save2) w4_cache_io(D, 2, B, cache + kW4C1, true, lane);
         w4_ph_edges(D, 2, B, A, d3, p3, lane);
     });
-    run([&](int lane) { w4_ph_rank(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_vkey(D, 3, A, b, lane); });
+    run([&](int lane) {
+        w4_ph_rank(D, 3, A, b, lane);
+        w4_ph_vkey(D, 3, A, b, lane);
+    });
     run([&](int lane) { w4_ph_vrank(D, 3, A, b, lane); });
     run([&](int lane) { w4_ph_norder(D, 3, A, b, lane); });
     run([&](int lane) { w4_ph_nsum(D, 3, A, b, lane); });

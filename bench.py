@@ -262,7 +262,7 @@ class Deletion:
         self.dense = self.dec.dense_layout(self.rx.shape[1], self.rx.device)
         self.kernel = "k_sc_del_dense" if self.dense else "k_sc_del"
         # n0 = 4, 64 .. 1024 trellises, no ones: the wave-per-task kernel (sc_del.hip's dispatch)
-        if (self.n0 == 4 and self.ones == 0 and 6 <= self.n - self.n0 <= (10 if a.del_wave >= 2 else 9) and a.del_wave != 0
+        if (self.n0 == 4 and self.ones == 0 and 6 <= self.n - self.n0 <= 10 and a.del_wave != 0
                 and (self.rx.shape[1] + 31) // 32 * 4 <= 32768):
             self.kernel = "k_sc_del_w4"
 

@@ -23,6 +23,10 @@ using namespace pcub;
 
 extern "C" int pcub_sc_dynamic_tiles(void);  // sc_bin.hip: work tiles from a counter
 
+namespace pcub {
+int del_w4_block(int tb);  // sc_del_w4.hip: threads a workgroup of del_kernel_w4(tb)
+}
+
 namespace {
 
 constexpr int kMaxOnes = 3;
@@ -217,16 +221,28 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
     const long long rw = ((long long)stride + 31) / 32;
     // n0 = 4 without ones (main_deletion's n = 12 .. 14): one wave a (trellis, depth-3 node) task, the
     // trellises in LDS (sc_del_w4.hip), codewords from a per-launch counter
-    // (at 1024 trellises, n = 14, the lane kernel is still faster: 10.0 k against 6.1 k cw/s -- the wave
-    // kernel's 64-value memoryless subtree spills; it takes them when asked, pcub_sc_set_deletion_wave(2))
     const int w4m = g_wave4.load(std::memory_order_relaxed);
-    if (!exp && n0 == 4 && ones == 0 && w4m && (n - n0 <= 9 || w4m == 2) && rw * 4 <= kW4MaxRxLds) {
+    if (!exp && n0 == 4 && ones == 0 && w4m && rw * 4 <= kW4MaxRxLds) {
         const DelKern wk = del_kernel_w4(n - n0, 0);
-        if (wk) {
+        // (the kernel's LDS is ~140 KB before the packed row: a row too long for what is left goes to the
+        // lane kernel)
+        int w4occ = 0;
+        if (wk && hipOccupancyMaxActiveBlocksPerMultiprocessor(&w4occ, wk, del_w4_block(n - n0), (size_t)(rw * 4)) != hipSuccess)
+            w4occ = 0;
+        if (wk && w4occ > 0) {
             A.rw = (int)rw;
             A.gate_id = w4m == 3 ? 1ull : 0ull;  // diagnostics: tasks skipped
             const size_t lds = (size_t)(rw * 4);
-            const long long grid = resident_grid(wk, lds, B);
+            // one resident workgroup a CU (k_sc_del_w4's launch bounds), at most one a codeword
+            const int wblk = del_w4_block(n - n0);
+            long long grid = B;
+            {
+                int dev = 0, cus = 0;
+                if (hipGetDevice(&dev) == hipSuccess &&
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 &&
+                    grid > (long long)cus * w4occ)
+                    grid = (long long)cus * w4occ;
+            }
             if (pcub_sc_dynamic_tiles()) {
                 const int rc = counter_slot(&A.wtiles, (hipStream_t)stream);
                 if (rc) return rc;
@@ -237,7 +253,7 @@ int launch_del(bool exp, const uint8_t* rx, const int32_t* rx_len, int64_t B, in
             hipError_t e = hipMallocAsync(&ws, (size_t)grid * ((size_t)1 << (n - n0)) * kW4Cache, (hipStream_t)stream);
             if (e != hipSuccess) return (int)e;
             A.leaf = (double*)ws;
-            hipLaunchKernelGGL(wk, dim3((unsigned)grid), dim3(kDelBlock), lds, (hipStream_t)stream, A);
+            hipLaunchKernelGGL(wk, dim3((unsigned)grid), dim3(wblk), lds, (hipStream_t)stream, A);
             const int rc = (int)hipGetLastError();
             e = hipFreeAsync(ws, (hipStream_t)stream);
             return rc ? rc : (int)e;
@@ -354,8 +370,8 @@ extern "C" int pcub_sc_set_deletion_lanes(int32_t g) {
 // of DESIGN 3.2.  Decisions are identical either way.  Returns the previous setting.
 extern "C" int pcub_sc_set_deletion_rate1(int32_t on) { return g_dense_rate1.exchange(on ? 1 : 0); }
 
-// Diagnostic (not part of the stable ABI; 2: the wave kernel at 512 / 1024 trellises too, 3: its tasks skipped,
-// a timing probe): 0 sends n0 = 4 decodes back to the lane-per-trellis kernel
+// Diagnostic (not part of the stable ABI; 3: the wave kernel with its tasks skipped, a timing probe): 0 sends
+// n0 = 4 decodes back to the lane-per-trellis kernel
 // k_sc_del instead of the wave-per-task kernel (sc_del_w4.hip); the A/B of DESIGN 3.2.  Decisions are
 // identical either way.  Returns the previous setting.
 extern "C" int pcub_sc_set_deletion_wave(int32_t on) { return g_wave4.exchange(on < 0 ? 0 : on > 3 ? 3 : on); }

@@ -24,8 +24,6 @@ namespace pcub {
 
 namespace {
 
-constexpr int kW4Waves = kDelBlock / 64;
-
 // run a phase on one lane of the wave, then make its LDS writes visible to the wave's other lanes
 struct W4WaveRun {
     int lane;
@@ -107,12 +105,18 @@ __device__ __forceinline__ int w4_info(const DelArgs& A, int kk, const unsigned 
     return total;
 }
 
-template <int TB, int MINB>
-__global__ __launch_bounds__(kDelBlock, MINB) void k_sc_del_w4(DelArgs A) {
+// WPB task waves a workgroup, one workgroup a CU: twelve (768 threads) up to 512 trellises, ten at
+// 1024 (the codeword's rows take more LDS).  One workgroup a CU asks the register allocator for 170
+// VGPRs: the task phases need ~120, and the memoryless subtree (wave 0, ~2 % of the time) spills
+// instead of pushing every wave to 256 -- at eight waves a CU the tasks ran 31 % slower than at twelve
+// (scripts/dbg/w4_tasks.hip).
+template <int TB, int WPB>
+__global__ __launch_bounds__(WPB * 64, 1) void k_sc_del_w4(DelArgs A) {
+    constexpr int BLK = WPB * 64;
     constexpr int T = 1 << TB;
     constexpr int LV = T / 16, NW = T / 64;
     constexpr int WPC = T / 2;  // x_hat words a codeword (16 T bits)
-    __shared__ W4Buf wb[kW4Waves];
+    __shared__ W4Buf wb[WPB];
     __shared__ double vm[T], vp0[T], vp1[T];
     __shared__ uint16_t hist[T], sy[T];
     __shared__ uint8_t sm[T];
@@ -135,12 +139,12 @@ __global__ __launch_bounds__(kDelBlock, MINB) void k_sc_del_w4(DelArgs A) {
         }
         if (cw >= A.B) break;
         // the received word, bit-packed; each trellis's segment (m > 16: no edges)
-        pack_rows<1, kDelBlock>(A, cw, rxb, lane);
-        for (int i = threadIdx.x; i < WPC; i += kDelBlock) infol[i] = 0u;
+        pack_rows<1, BLK>(A, cw, rxb, lane);
+        for (int i = threadIdx.x; i < WPC; i += BLK) infol[i] = 0u;
         __syncthreads();
         int len = A.rx_len[cw];
         len = len < 0 ? 0 : (len > A.stride ? A.stride : len);
-        for (int t = threadIdx.x; t < T; t += kDelBlock) {
+        for (int t = threadIdx.x; t < T; t += BLK) {
             int s, m;
             segment_of_packed(rxb, len, TB, t, s, m);
             uint32_t y = 0;
@@ -168,7 +172,7 @@ __global__ __launch_bounds__(kDelBlock, MINB) void k_sc_del_w4(DelArgs A) {
                     have2 = k >> 1;
                 }
 #pragma unroll 1
-                for (int t = wv; t < T; t += kW4Waves) {
+                for (int t = wv; t < T; t += WPB) {
                     // the task's segment and history are wave-uniform: scalar registers
                     W4Dims D;
                     D.set(__builtin_amdgcn_readfirstlane((int)sm[t]), (uint32_t)__builtin_amdgcn_readfirstlane((int)sy[t]),
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(kDelBlock, MINB) void k_sc_del_w4(DelArgs A) {
             // the minus node, then every position's plus row by its decision, then the plus node
             w4_subtree<TB>(A, vm, km, xb, xub);
             ib += w4_info<T>(A, km, xub, infol, ib);
-            for (int p = threadIdx.x; p < T; p += kDelBlock) {
+            for (int p = threadIdx.x; p < T; p += BLK) {
                 const uint32_t x = (uint32_t)(xb[p >> 4] >> (p & 15)) & 1u;
                 xmb[p] = (uint8_t)x;
                 vm[p] = x ? vp1[p] : vp0[p];
@@ -194,7 +198,7 @@ __global__ __launch_bounds__(kDelBlock, MINB) void k_sc_del_w4(DelArgs A) {
             __syncthreads();
             w4_subtree<TB>(A, vm, kp, xb, xub);
             ib += w4_info<T>(A, kp, xub, infol, ib);
-            for (int t = threadIdx.x; t < T; t += kDelBlock) {
+            for (int t = threadIdx.x; t < T; t += BLK) {
                 const int p = (int)bitrev((uint32_t)t, TB);
                 const uint32_t xp = (uint32_t)(xb[p >> 4] >> (p & 15)) & 1u;
                 hist[t] = (uint16_t)(hist[t] | ((uint32_t)xmb[p] << km) | (xp << kp));
@@ -203,10 +207,10 @@ __global__ __launch_bounds__(kDelBlock, MINB) void k_sc_del_w4(DelArgs A) {
         }
         // x_hat: trellis t's slice is natural positions [16 t, 16 t + 16)
         if (A.xhat)
-            for (int i = threadIdx.x; i < WPC; i += kDelBlock)
+            for (int i = threadIdx.x; i < WPC; i += BLK)
                 A.xhat[(long long)i * A.B + cw] = w4_enc16(hist[2 * i]) | (w4_enc16(hist[2 * i + 1]) << 16);
         if (A.info)
-            for (int i = threadIdx.x; i < (ib + 31) / 32; i += kDelBlock) A.info[(long long)i * A.B + cw] = infol[i];
+            for (int i = threadIdx.x; i < (ib + 31) / 32; i += BLK) A.info[(long long)i * A.B + cw] = infol[i];
         __syncthreads();  // rxb / sm / hist / infol are rewritten by the next codeword
     }
 }
@@ -214,17 +218,18 @@ __global__ __launch_bounds__(kDelBlock, MINB) void k_sc_del_w4(DelArgs A) {
 }  // namespace
 
 DelKern del_kernel_w4(int tb, int alt) {
-    // two workgroups a CU (eight waves): the register allocator must fit the memoryless subtree and the
-    // task phases into 256 VGPRs; unbounded, the subtree's register tree pushed TB = 8 to one wave a SIMD
     (void)alt;
     switch (tb) {
-        case 6: return k_sc_del_w4<6, 2>;
-        case 7: return k_sc_del_w4<7, 2>;
-        case 8: return k_sc_del_w4<8, 2>;
-        case 9: return k_sc_del_w4<9, 2>;
-        case 10: return k_sc_del_w4<10, 2>;
+        case 6: return k_sc_del_w4<6, 12>;
+        case 7: return k_sc_del_w4<7, 12>;
+        case 8: return k_sc_del_w4<8, 12>;
+        case 9: return k_sc_del_w4<9, 12>;
+        case 10: return k_sc_del_w4<10, 10>;
         default: return nullptr;
     }
 }
+
+// threads a workgroup of del_kernel_w4(tb)
+int del_w4_block(int tb) { return (tb == 10 ? 10 : 12) * 64; }
 
 }  // namespace pcub

@@ -18,4 +18,7 @@ run c2 "--steps 10 --warmup 3" || exit 1
 run c5 "--workload deletion --steps 10 --warmup 3" || exit 1
 run d12 "--workload deletion --n 12 --batch 32768 --steps 3 --warmup 1 --no-cpu" || exit 1
 run d13 "--workload deletion --n 13 --batch 16384 --steps 3 --warmup 1 --no-cpu" || exit 1
+run d14 "--workload deletion --n 14 --batch 8192 --steps 3 --warmup 1 --no-cpu" || exit 1
+run d12_lane "--workload deletion --n 12 --batch 8192 --steps 2 --warmup 1 --no-cpu --del-wave 0" || exit 1
+run d14_lane "--workload deletion --n 14 --batch 4096 --steps 2 --warmup 1 --no-cpu --del-wave 0" || exit 1
 exit 0

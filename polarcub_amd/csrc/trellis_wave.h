@@ -511,30 +511,119 @@ PCUB_HD void w4_ph_ndiv(const W4Dims& D, int dc, const W4View& C, const W4Buf& b
     }
 }
 
-// the three collapsed rows of the depth-3 trellis (lanes 0, 1, 2: minus, plus after 0, plus after 1)
-PCUB_HD void w4_ph_collapse(const W4Dims& D, const W4View& C, W4Buf& b, int lane) {
+// ---- depth 3 (the length-2 trellis) and its collapse, without the generic phases ----
+//
+// Its layer 0 leaves the start vertex only and its layer 1 enters the end vertex m only, so every edge
+// is (0 -> w, x) or (w -> m, x) for the <= 9 middle vertices w: the creation order that matters is the
+// label order of each (0, w) and (w, m) pair and the key order of layer 0's edges, the middle vertices'
+// insertion order is the rank of their (phase, least key), and each normaliser is a short ordered sum.
+// Same values and orders as the generic phases (w4_check compares them with the Trel walk).
+
+// F1: middle-vertex keys (lanes 0..8); layer 0's edges scattered by key order per label (lanes 16..)
+PCUB_HD void w4_ph_f1(const W4Dims& D, const W4View& C, W4Buf& b, int lane) {
+    const int NA = D.na(3), AM = D.amin(3);
+    const int wlo = D.lo(8), nw = w4_nu(D, 8);
+    if (lane < nw) {
+        const int w = wlo + lane;
+        uint32_t vk = kW4NoV;
+        const int a1 = w - AM;
+        if (a1 >= 0 && a1 < NA) {
+            const uint2 q = *reinterpret_cast<const uint2*>(C.k + 2 * a1);
+            const uint32_t k0 = q.x < q.y ? q.x : q.y;
+            if (k0 != kW4None) vk = k0;
+        }
+        if (vk == kW4NoV) {
+            const int a2 = D.m - w - AM;
+            if (a2 >= 0 && a2 < NA) {
+                const uint2 q = *reinterpret_cast<const uint2*>(C.k + D.sl(3) + (lane * NA + a2) * 2);
+                const uint32_t k1 = q.x < q.y ? q.x : q.y;
+                if (k1 != kW4None) vk = 0x80000000u | k1;
+            }
+        }
+        b.vkey[0][lane] = vk;
+    }
+    int e0, e1;  // layer 0's enumerated advance offsets (the slots outside are never written)
+    w4_arange(D, 3, 0, 0, e0, e1);
+    if (lane >= 16 && lane < 16 + 2 * NA) {
+        const int i = lane - 16, ao = i >> 1, x = i & 1;
+        if (ao >= e0 && ao <= e1) {
+            const uint32_t k = C.k[2 * ao + x];
+            if (k != kW4None) {
+                int n = 0;
+                for (int a2 = e0; a2 <= e1; ++a2) n += C.k[2 * a2 + x] < k ? 1 : 0;
+                C.tmp[x * 16 + n] = C.p[2 * ao + x];
+            }
+        }
+    }
+    if (lane >= 48 && lane < 50) {  // layer 0's edge count per label
+        const int x = lane - 48;
+        int n = 0;
+        for (int a2 = e0; a2 <= e1; ++a2) n += C.k[2 * a2 + x] != kW4None ? 1 : 0;
+        b.ncnt[0][x] = (uint32_t)n;
+    }
+}
+
+// F2: middle-vertex insertion order (lanes 0..8); layer 0's normaliser sums (lanes 16, 17)
+PCUB_HD void w4_ph_f2(const W4Dims& D, const W4View& C, W4Buf& b, int lane) {
+    const int nw = w4_nu(D, 8);
+    if (lane < nw) {
+        const uint32_t vk = b.vkey[0][lane];
+        int r = 0, nv = 0;
+        for (int t = 0; t < nw; ++t) {
+            const uint32_t o = b.vkey[0][t];
+            r += o < vk ? 1 : 0;
+            nv += o != kW4NoV ? 1 : 0;
+        }
+        if (vk != kW4NoV) C.vo[1][r] = (uint8_t)lane;
+        if (lane == 0) C.nv[1] = (uint8_t)nv;
+    }
+    if (lane == 16 || lane == 17) {
+        const int x = lane - 16;
+        const int n = (int)b.ncnt[0][x];
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += C.tmp[x * 16 + i];
+        b.sums[0][x] = s;
+    }
+}
+
+// F3: layer 1's normaliser (vertices in insertion order, one edge a label each) and the three
+// collapsed rows from the normalised edges (lanes 0, 1, 2: minus, plus after 0, plus after 1)
+PCUB_HD void w4_ph_f3(const W4Dims& D, const W4View& C, W4Buf& b, int lane) {
     if (lane >= 3) return;
-    const int NA = D.na(3), SL = D.sl(3), AM = D.amin(3);
+    const int NA = D.na(3), AM = D.amin(3);
     const int wlo = D.lo(8);
-    double m0 = 0.0, m1 = 0.0;
     const int nv1 = C.nv[1];
+    const int L1 = D.sl(3);  // layer 1's first slot
+    double t0 = 0.0, t1 = 0.0;
+    for (int r = 0; r < nv1; ++r) {
+        const int wo = C.vo[1][r];
+        const int a2 = D.m - (wlo + wo) - AM;
+        if (a2 < 0 || a2 >= NA) continue;
+        const int ib = L1 + (wo * NA + a2) * 2;
+        if (C.k[ib] != kW4None) t0 += C.p[ib];
+        if (C.k[ib + 1] != kW4None) t1 += C.p[ib + 1];
+    }
+    double d0 = b.sums[0][0] >= b.sums[0][1] ? b.sums[0][0] : b.sums[0][1];
+    if (d0 == 0.0) d0 = 1.0;
+    double d1 = t0 >= t1 ? t0 : t1;
+    if (d1 == 0.0) d1 = 1.0;
+    double m0 = 0.0, m1 = 0.0;
     for (int r = 0; r < nv1; ++r) {
         const int wo = C.vo[1][r];
         const int w = wlo + wo;
         const int a1 = w - AM, a2 = D.m - w - AM;
         if (a1 < 0 || a1 >= NA || a2 < 0 || a2 >= NA) continue;
-        const int ia = a1 * 2;                       // layer 0, from vertex 0 (offset 0)
-        const int ib = SL + (wo * NA + a2) * 2;      // layer 1, to vertex m
-        const int ca0 = C.c[ia], ca1 = C.c[ia + 1], cb0 = C.c[ib], cb1 = C.c[ib + 1];
-        const int fa = ca1 < ca0 ? 1 : 0, fb = cb1 < cb0 ? 1 : 0;
+        const int ia = 2 * a1, ib = L1 + (wo * NA + a2) * 2;
+        const uint32_t ka0 = C.k[ia], ka1 = C.k[ia + 1], kb0 = C.k[ib], kb1 = C.k[ib + 1];
+        const int fa = ka1 < ka0 ? 1 : 0, fb = kb1 < kb0 ? 1 : 0;
         for (int t = 0; t < 2; ++t) {
             const int la = fa ^ t;
-            if ((la ? ca1 : ca0) == kW4NoC) continue;
-            const double pa = C.p[ia + la];
+            if ((la ? ka1 : ka0) == kW4None) continue;
+            const double pa = C.p[ia + la] / d0;
             for (int q = 0; q < 2; ++q) {
                 const int lb = fb ^ q;
-                if ((lb ? cb1 : cb0) == kW4NoC) continue;
-                const double prob = pa * C.p[ib + lb];
+                if ((lb ? kb1 : kb0) == kW4None) continue;
+                const double prob = pa * (C.p[ib + lb] / d1);
                 const int ml = la ^ lb;
                 int x = ml;
                 if (lane > 0) {
@@ -651,20 +740,14 @@ PCUB_HD void w4_task(const Run& run, W4Buf& b, const W4Dims& D, int k, uint32_t 
     } else {
         run([&](int lane) { w4_cache_io(D, 2, B, cache + kW4C1, false, lane); });
     }
-    // depth 3 (region A again)
+    // depth 3 (region A again) and the rows
     run([&](int lane) {
         if (mode & kW4Save2) w4_cache_io(D, 2, B, cache + kW4C1, true, lane);
         w4_ph_edges(D, 2, B, A, d3, p3, lane);
     });
-    run([&](int lane) {
-        w4_ph_rank(D, 3, A, b, lane);
-        w4_ph_vkey(D, 3, A, b, lane);
-    });
-    run([&](int lane) { w4_ph_vrank(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_norder(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_nsum(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_ndiv(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_collapse(D, A, b, lane); });
+    run([&](int lane) { w4_ph_f1(D, A, b, lane); });
+    run([&](int lane) { w4_ph_f2(D, A, b, lane); });
+    run([&](int lane) { w4_ph_f3(D, A, b, lane); });
 }
 
 }  // namespace pcub

@@ -26,7 +26,7 @@ struct WR {
 };
 
 // w4_task up to a stage: 1 = depth-1 edges, 2 = depth 1 complete, 3 = + depth-2 edges, 4 = depth 2
-// complete, 5 = + depth-3 edges, 6 = depth 3 complete, 7 = everything
+// complete, 5 = + depth-3 edges, 6 = + the middle-vertex order and layer 0's normaliser, 7 = everything
 template <int STOP, class Run>
 __device__ __forceinline__ void w4_task_upto(const Run& run, W4Buf& b, const W4Dims& D, int k, uint32_t hist) {
     if (D.m > kW4L) {
@@ -58,14 +58,10 @@ __device__ __forceinline__ void w4_task_upto(const Run& run, W4Buf& b, const W4D
     if (STOP == 4) return;
     run([&](int lane) { w4_ph_edges(D, 2, B, A, d3, p3, lane); });
     if (STOP == 5) return;
-    run([&](int lane) { w4_ph_rank(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_vkey(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_vrank(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_norder(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_nsum(D, 3, A, b, lane); });
-    run([&](int lane) { w4_ph_ndiv(D, 3, A, b, lane); });
+    run([&](int lane) { w4_ph_f1(D, A, b, lane); });
+    run([&](int lane) { w4_ph_f2(D, A, b, lane); });
     if (STOP == 6) return;
-    run([&](int lane) { w4_ph_collapse(D, A, b, lane); });
+    run([&](int lane) { w4_ph_f3(D, A, b, lane); });
 }
 
 template <int STOP>
@@ -116,10 +112,11 @@ __global__ __launch_bounds__(WPB * 64, MINB) void k_tasks(const uint32_t* seg, c
 }
 
 template <int WPB, int MINB>
-static void run(const char* name, const uint32_t* seg, const uint16_t* hist, double* rows, long long n) {
+static void run(const char* name, const uint32_t* seg, const uint16_t* hist, double* rows, long long n, int cap = 0) {
     int cus = 0, occ = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_tasks<WPB, MINB>, WPB * 64, 0);
+    if (cap > 0 && cap < occ) occ = cap;
     const long long grid = (long long)cus * occ;
     hipEvent_t a, b;
     hipEventCreate(&a);
@@ -162,6 +159,9 @@ int main(int argc, char** argv) {
     hipMemcpy(dseg, seg.data(), n * 4, hipMemcpyHostToDevice);
     hipMemcpy(dhist, hist.data(), n * 2, hipMemcpyHostToDevice);
     run<1, 1>("1 wave/WG", dseg, dhist, drows, n);
+    run<1, 1>("1 wave/WG, 4 a CU", dseg, dhist, drows, n, 4);
+    run<1, 1>("1 wave/WG, 8 a CU", dseg, dhist, drows, n, 8);
+    run<1, 1>("1 wave/WG, 10 a CU", dseg, dhist, drows, n, 10);
     stage<1>(dseg, dhist, drows, n);
     stage<2>(dseg, dhist, drows, n);
     stage<3>(dseg, dhist, drows, n);

@@ -124,6 +124,7 @@ __global__ __launch_bounds__(WPB * 64, 1) void k_sc_del_w4(DelArgs A) {
     __shared__ unsigned long long xb[LV], xub[NW];
     __shared__ uint32_t infol[WPC];
     __shared__ long long s_next;
+    __shared__ int s_task[8];  // node k's next task (the waves take the codeword's trellises in turn)
     extern __shared__ uint32_t rxb[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // this workgroup's trellis caches (the launcher's workspace, kW4Cache bytes a trellis), or none
@@ -157,6 +158,7 @@ __global__ __launch_bounds__(WPB * 64, 1) void k_sc_del_w4(DelArgs A) {
             sy[t] = (uint16_t)y;
             hist[t] = 0;
         }
+        if (threadIdx.x < 8) s_task[threadIdx.x] = 0;
         __syncthreads();
         int ib = 0;  // information bits so far
         int have1 = -1, have2 = -1;  // the depth-1 (k >> 2) / depth-2 (k >> 1) trellises in the cache
@@ -171,8 +173,20 @@ __global__ __launch_bounds__(WPB * 64, 1) void k_sc_del_w4(DelArgs A) {
                     if (mode & kW4Save1) have1 = k >> 2;
                     have2 = k >> 1;
                 }
+                // up to 256 trellises the tasks come from a counter, not a fixed stride: their costs differ
+                // (segment lengths), and the node's subtree waits for the slowest wave (n = 12: 60.3 ->
+                // 68.2 k cw/s); at 512 / 1024 the fixed stride measured faster (32.7 / 13.5 k against 31.5 /
+                // 10.1 k), so it stays there
+                constexpr bool kDyn = TB <= 8;
 #pragma unroll 1
-                for (int t = wv; t < T; t += WPB) {
+                for (int ts = wv;; ts += WPB) {
+                    int t = ts;
+                    if constexpr (kDyn) {
+                        t = 0;
+                        if (lane == 0) t = atomicAdd(&s_task[k], 1);
+                        t = __builtin_amdgcn_readfirstlane(t);
+                    }
+                    if (t >= T) break;
                     // the task's segment and history are wave-uniform: scalar registers
                     W4Dims D;
                     D.set(__builtin_amdgcn_readfirstlane((int)sm[t]), (uint32_t)__builtin_amdgcn_readfirstlane((int)sy[t]),
